@@ -1,0 +1,141 @@
+/*
+ * dtc.h — C ABI of the MI355X DTC autocorrelator engine (libdtc_hip.so).
+ *
+ * This ABI replaces the one call the reference makes into its execution
+ * engine for the DTC sweep:
+ *
+ *   backend = AerSimulator(noise_model=noise_model, device="GPU",
+ *                          cuStateVec_enable=True)          fast.py:156
+ *   backend.run(circ_tnoise, shots=1024).result()
+ *          .get_counts(circ_tnoise)                          fast.py:211-212
+ *   compute_z_expectation(counts, 1)[0]                      fast.py:92-109,213
+ *
+ * (fast.py = autocorr-delta-a-single-qiskit-fast.py; the same call appears at
+ *  ...-polarization.py:219, ...-circular-polarization.py:241,
+ *  ...-controlled-g.py:305, ...-g-optimization.py:309, ...-shots.py:214.)
+ *
+ * Aer runs one (L+1)-qubit circuit per time point t.  The engine instead runs
+ * the folded L-qubit model: every time point of the
+ * forward sweep comes from one trajectory, and every echo point t branches
+ * off the forward state at t.  Results per trajectory are the ancilla
+ * expectation value  a_r(t) = (1-p)^n_anc * z_j(init_r) * <Z_j>_r(t),
+ * whose mean over trajectories is the expectation of
+ * (n0 - n1)/shots in the reference.
+ *
+ * Conventions
+ *  - Site i of the spin chain is bit i of the amplitude index (qiskit
+ *    little-endian, circuit qubit i+1; the ancilla is folded away).
+ *  - complex128 amplitudes, interleaved (re, im).
+ *  - Kick matrices are complex 2x2, row-major, interleaved:
+ *    {m00.re, m00.im, m01.re, m01.im, m10.re, m10.im, m11.re, m11.im}.
+ *  - All host arrays are C-contiguous and owned by the caller.
+ *  - Return value 0 = success; negative = error, message via
+ *    dtc_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *  - Calls are synchronous (return after a stream sync).  One dtc_ctx per
+ *    device per host thread; a ctx is not re-entrant.
+ */
+#ifndef DTC_H
+#define DTC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DTC_ABI_VERSION 1
+
+/* error codes */
+#define DTC_OK 0
+#define DTC_EINVAL (-1)   /* bad argument                          */
+#define DTC_EHIP (-2)     /* HIP runtime error                     */
+#define DTC_ENOMEM (-3)   /* device allocation failed              */
+#define DTC_ENODEV (-4)   /* no usable gfx950 device               */
+
+typedef struct dtc_ctx dtc_ctx;
+
+/* One disorder sweep (fast.py:41-74 argparse + disorder load, and the circuit
+ * family of fast.py:111-147 / ...-polarization.py:110-142 /
+ * ...-controlled-g.py:196-241). */
+typedef struct dtc_problem {
+  int32_t L;           /* sites (fast.py --L)                              */
+  int32_t T;           /* time points t = 0..T-1 (fast.py:48-51, --tf)      */
+  int32_t n_inst;      /* disorder instances (fast.py --inst)              */
+  int32_t probe_site;  /* j = int(L/2) (fast.py:221)                        */
+  int32_t t_offset;    /* periods applied at t = t + t_offset: 0 for fast.py,
+                          1 for controlled-g.py:416,467                    */
+  int32_t n_sub;       /* noisy kick sub-gates per site per period:
+                          1 (x, y), 2 (xy, yx, circular)                   */
+  uint64_t init_mask;  /* Z-basis product state: bit i set = X on site i
+                          (neel: fast.py:127-130)                          */
+  const double* h;     /* [n_inst][L]   on-site RZ(h_i) angles              */
+  const double* phi;   /* [n_inst][L-1] bond RZZ(phi_i) angles              */
+  const double* kick;  /* [n_periods][L][n_sub][8] complex 2x2 kick gates,
+                          row p = the (p+1)-th forward period,
+                          n_periods = T - 1 + t_offset                     */
+  int32_t want_fwd;    /* compute the forward autocorrelator              */
+  int32_t want_echo;   /* compute the echo autocorrelator                 */
+  int32_t batch;       /* states per device batch, 0 = automatic          */
+  int32_t reserved;
+} dtc_problem;
+
+/* Noise model (fast.py:76-86): depolarizing_error(p, 1) after every noisy
+ * single-qubit gate (u2/u3 = kick gates, neel X prep, and n_anc ancilla
+ * u2 gates).  p = 0 or use_noise = 0 means ideal. */
+typedef struct dtc_noise {
+  double p;
+  int32_t n_anc;       /* noisy ancilla gates folded as (1-p)^n_anc: 6   */
+  int32_t reserved;
+} dtc_noise;
+
+/* Context management. device = HIP device ordinal. */
+int dtc_open(int32_t device, dtc_ctx** out);
+int dtc_close(dtc_ctx* ctx);
+const char* dtc_last_error(void);
+int32_t dtc_abi_version(void);
+
+/* Full sweep for trajectories [traj_offset, traj_offset + n_traj) of every
+ * instance.  Per-trajectory outputs (caller averages; see header comment):
+ *   fwd   [n_inst][n_traj][T]     (nullable if !want_fwd)
+ *   echo  [n_inst][n_traj][T]     (nullable if !want_echo)
+ *   zsite [n_inst][n_traj][T][L]  forward per-site <Z_i>(t), nullable
+ * Replaces the get_instances/get_single_out loops (fast.py:217-239) over
+ * backend.run (fast.py:211).  The noise RNG is Philox4x32-10 keyed by seed
+ * and counted by (global trajectory, stream, period, site, sub-gate), so
+ * results do not depend on batching or on how trajectories are sharded. */
+int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                 uint64_t seed, int64_t traj_offset, int32_t n_traj,
+                 double* fwd, double* echo, double* zsite);
+
+/* Unit-test hook: apply n_periods Floquet periods to one host state vector
+ * of 2^L complex128 amplitudes (in/out).  Forward: periods first_period,
+ * first_period+1, ... (1-based rows of prob->kick), RNG stream `stream`,
+ * RNG period counter = period.  Inverse (fast.py:140-143): periods
+ * first_period, first_period-1, ..., each U_F^-1, RNG period counter =
+ * step k = 1..n_periods.  zsite_out (nullable) receives [norm, <Z_0>..<Z_{L-1}>]
+ * of the final state. */
+int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                      uint64_t seed, int32_t inst, int64_t traj, uint32_t stream,
+                      int32_t first_period, int32_t n_periods, int32_t inverse,
+                      double* state, double* zsite_out);
+
+/* Profiling: when enabled, every kernel launch is bracketed by HIP events on
+ * the ctx stream and accumulated per kernel kind. */
+#define DTC_KERNEL_LO_PASS 0   /* fused RZZ+RZ diagonal + low-site kick pass */
+#define DTC_KERNEL_HI_PASS 1   /* high-site kick pass                        */
+#define DTC_KERNEL_REDUCE 2    /* per-state observable reduction             */
+#define DTC_KERNEL_INIT 3      /* basis-state preparation                    */
+#define DTC_KERNEL_KINDS 4
+int dtc_set_profiling(dtc_ctx* ctx, int32_t on);
+int dtc_kernel_stats(dtc_ctx* ctx, int32_t kind, int64_t* launches,
+                     double* total_ms, double* total_bytes);
+int dtc_reset_stats(dtc_ctx* ctx);
+
+/* Device properties for reports. */
+int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,
+                    double* hbm_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DTC_H */

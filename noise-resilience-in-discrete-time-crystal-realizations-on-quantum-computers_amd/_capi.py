@@ -1,0 +1,137 @@
+"""ctypes binding of the C ABI in ``include/dtc.h`` (``lib/libdtc_hip.so``).
+
+The product path has exactly one implementation: the gfx950 HIP kernels in
+``csrc/``.  If the shared library is missing or no gfx950 device is present
+every entry point raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
+
+# Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
+EXPORTED_SYMBOLS = (
+    "dtc_open",
+    "dtc_close",
+    "dtc_last_error",
+    "dtc_abi_version",
+    "dtc_autocorr",
+    "dtc_apply_periods",
+    "dtc_set_profiling",
+    "dtc_kernel_stats",
+    "dtc_reset_stats",
+    "dtc_device_info",
+)
+
+KERNEL_LO_PASS = 0
+KERNEL_HI_PASS = 1
+KERNEL_REDUCE = 2
+KERNEL_INIT = 3
+KERNEL_NAMES = {
+    KERNEL_LO_PASS: "pass_kernel<diag>  (fused RZZ+RZ diagonal + sites 0..11 kick)",
+    KERNEL_HI_PASS: "pass_kernel<none>  (kick on sites >= 12)",
+    KERNEL_REDUCE: "reduce_kernel",
+    KERNEL_INIT: "set_basis_kernel",
+}
+
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+class DtcProblem(ctypes.Structure):
+    """Mirror of ``dtc_problem`` (include/dtc.h)."""
+
+    _fields_ = [
+        ("L", ctypes.c_int32),
+        ("T", ctypes.c_int32),
+        ("n_inst", ctypes.c_int32),
+        ("probe_site", ctypes.c_int32),
+        ("t_offset", ctypes.c_int32),
+        ("n_sub", ctypes.c_int32),
+        ("init_mask", ctypes.c_uint64),
+        ("h", _dp),
+        ("phi", _dp),
+        ("kick", _dp),
+        ("want_fwd", ctypes.c_int32),
+        ("want_echo", ctypes.c_int32),
+        ("batch", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class DtcNoise(ctypes.Structure):
+    """Mirror of ``dtc_noise`` (include/dtc.h)."""
+
+    _fields_ = [
+        ("p", ctypes.c_double),
+        ("n_anc", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class DtcError(RuntimeError):
+    """Raised when a C-ABI call returns a negative code."""
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libdtc_hip.so and declare argument types.  Raises if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = path or os.environ.get("DTC_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise DtcError(
+                f"HIP extension not built: {p} is missing (run `make` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'`)"
+            )
+        lib = ctypes.CDLL(p)
+        P = ctypes.POINTER
+        lib.dtc_open.argtypes = [ctypes.c_int32, P(ctypes.c_void_p)]
+        lib.dtc_close.argtypes = [ctypes.c_void_p]
+        lib.dtc_last_error.restype = ctypes.c_char_p
+        lib.dtc_abi_version.restype = ctypes.c_int32
+        lib.dtc_autocorr.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), ctypes.c_uint64, ctypes.c_int64,
+            ctypes.c_int32, _dp, _dp, _dp,
+        ]
+        lib.dtc_apply_periods.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), ctypes.c_uint64, ctypes.c_int32,
+            ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+            _dp, _dp,
+        ]
+        lib.dtc_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        lib.dtc_kernel_stats.argtypes = [
+            ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int64), _dp, _dp,
+        ]
+        lib.dtc_reset_stats.argtypes = [ctypes.c_void_p]
+        lib.dtc_device_info.argtypes = [
+            ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, P(ctypes.c_int32), _dp,
+        ]
+        for name in EXPORTED_SYMBOLS:
+            if name not in ("dtc_last_error", "dtc_abi_version"):
+                getattr(lib, name).restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.dtc_last_error().decode() if _lib is not None else "unknown"
+        raise DtcError(f"libdtc_hip error {rc}: {msg}")
+
+
+def as_dptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_dp)

@@ -1,0 +1,341 @@
+// dtc_kernels.hip — gfx950 (CDNA4) kernels for the DTC Floquet period.
+//
+// One Floquet period of the reference (create_UF_subcircuit, fast.py:111-121):
+//   RX(pi g) on every site  ->  RZZ(phi_i) on even then odd bonds  ->
+//   RZ(h_i) on every site,
+// with a Pauli draw after every kick gate (depolarizing noise on u3,
+// fast.py:84-86).  The inverse period (fast.py:140-143) is RZ(-h), RZZ(-phi),
+// RX(-pi g) with noise after each kick.  Single-site kicks on different sites
+// commute, and RZZ/RZ are one diagonal D(x), so a period is
+//     D . K_lo . K_hi      (forward)      K'_hi . K'_lo . D^*   (inverse)
+// where K_lo acts on sites 0..11 and K_hi on the rest.  Each factor group is
+// one streaming pass over the state: a workgroup loads a 4096-amplitude tile
+// (16 amplitudes per lane, coalesced 16-B loads), applies the 2x2 kick of
+// every site whose bit lies in the tile as register butterflies, re-layouts
+// the tile through 64 KiB of bank-conflict-free (XOR-swizzled) LDS between
+// 4-site rounds, applies the diagonal from per-instance LDS factor tables,
+// optionally reduces |a|^2 Z_i for the autocorrelator, and stores the tile
+// back.  Memory-bound by design: 32 B of HBM traffic per amplitude per pass,
+// no MFMA (complex128 butterflies are not GEMM-shaped).
+#include "dtc_kernels.h"
+#include "dtc_rng.h"
+
+namespace dtc {
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// (u, v) <- (m00 u + m01 v, m10 u + m11 v)
+__device__ __forceinline__ void butterfly(double2& u, double2& v, const double2* m) {
+  const double2 m00 = m[0], m01 = m[1], m10 = m[2], m11 = m[3];
+  double2 nu, nv;
+  nu.x = m00.x * u.x - m00.y * u.y + m01.x * v.x - m01.y * v.y;
+  nu.y = m00.x * u.y + m00.y * u.x + m01.x * v.y + m01.y * v.x;
+  nv.x = m10.x * u.x - m10.y * u.y + m11.x * v.x - m11.y * v.y;
+  nv.y = m10.x * u.y + m10.y * u.x + m11.x * v.y + m11.y * v.x;
+  u = nu;
+  v = nv;
+}
+
+// m <- P m for Pauli code (1 X, 2 Y, 3 Z)
+__device__ __forceinline__ void pauli_left(double2* m, int pauli) {
+  if (pauli == 1) {
+    double2 t0 = m[0], t1 = m[1];
+    m[0] = m[2]; m[1] = m[3]; m[2] = t0; m[3] = t1;
+  } else if (pauli == 2) {
+    // Y = [[0, -i], [i, 0]]: row0 <- -i row1, row1 <- i row0
+    double2 r00 = m[0], r01 = m[1];
+    m[0] = make_double2(m[2].y, -m[2].x);
+    m[1] = make_double2(m[3].y, -m[3].x);
+    m[2] = make_double2(-r00.y, r00.x);
+    m[3] = make_double2(-r01.y, r01.x);
+  } else if (pauli == 3) {
+    m[2] = make_double2(-m[2].x, -m[2].y);
+    m[3] = make_double2(-m[3].x, -m[3].y);
+  }
+}
+
+// c <- a b (2x2 complex)
+__device__ __forceinline__ void mat_mul(double2* c, const double2* a, const double2* b) {
+  double2 r[4];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) {
+      double2 x = cmul(a[2 * i + 0], b[0 + j]);
+      double2 y = cmul(a[2 * i + 1], b[2 + j]);
+      r[2 * i + j] = make_double2(x.x + y.x, x.y + y.y);
+    }
+  for (int k = 0; k < 4; ++k) c[k] = r[k];
+}
+
+// Noisy kick of one site for one period: M = P_n G_n ... P_1 G_1.
+__device__ void build_site_kick(const PassArgs& A, int site, uint64_t traj, double2* m) {
+  m[0] = make_double2(1.0, 0.0);
+  m[1] = make_double2(0.0, 0.0);
+  m[2] = make_double2(0.0, 0.0);
+  m[3] = make_double2(1.0, 0.0);
+  for (int q = 0; q < A.n_sub; ++q) {
+    const int qq = A.inverse ? (A.n_sub - 1 - q) : q;
+    const double2* gp = A.kick + (((int64_t)A.kick_row * A.L_real + site) * A.n_sub + qq) * 4;
+    double2 gm[4];
+    if (A.inverse) {  // G^dagger
+      gm[0] = make_double2(gp[0].x, -gp[0].y);
+      gm[1] = make_double2(gp[2].x, -gp[2].y);
+      gm[2] = make_double2(gp[1].x, -gp[1].y);
+      gm[3] = make_double2(gp[3].x, -gp[3].y);
+    } else {
+      gm[0] = gp[0]; gm[1] = gp[1]; gm[2] = gp[2]; gm[3] = gp[3];
+    }
+    mat_mul(m, gm, m);
+    if (A.noisy) {
+      int p = sample_pauli(A.seed, traj, A.stream, A.rng_period, (uint32_t)site, (uint32_t)q,
+                           A.thr1, A.thr2, A.thr3);
+      pauli_left(m, p);
+    }
+  }
+}
+
+// Tile layouts: register r of lane-thread t holds tile index Y(t, r).
+// Layout 2: registers = tile bits 8..11, threads = bits 0..7 (coalesced).
+// Layout 1: registers = tile bits 4..7.  Layout 0: registers = bits 0..3.
+__device__ __forceinline__ int tile_y(int layout, int t, int r) {
+  if (layout == 2) return t | (r << 8);
+  if (layout == 1) return (t & 15) | (r << 4) | ((t >> 4) << 8);
+  return r | (t << 4);
+}
+
+// XOR swizzle over 16-B slots: conflict-free ds_write_b128 / ds_read_b128 for
+// every layout transition used here (MI355X_MICROARCH.md §LDS lane groups).
+__device__ __forceinline__ int lds_slot(int y) { return y ^ ((y >> 4) & 15); }
+
+template <int N>
+__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const double2 (*s_mat)[4],
+                                             int act) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 4 * N + q;
+    if (act & (1 << k)) {
+      double2 m[4];
+      m[0] = s_mat[k][0]; m[1] = s_mat[k][1]; m[2] = s_mat[k][2]; m[3] = s_mat[k][3];
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        if (!(r & (1 << q))) butterfly(v[r], v[r | (1 << q)], m);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ double2 diag_phase(const double2* s_diag, int n_chunks, int64_t x) {
+  double2 ph = s_diag[x & 63];
+  for (int k = 1; k < n_chunks; ++k) {
+    ph = cmul(ph, s_diag[k * 64 + ((x >> (kChunkBits * k)) & 63)]);
+  }
+  return ph;
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+template <int DIAG, int MEAS>
+__global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
+  __shared__ double2 s_tile[kTile];
+  __shared__ double2 s_diag[DIAG != kDiagNone ? kMaxChunks * 64 : 1];
+  __shared__ double2 s_mat[kTileBits][4];
+  __shared__ double s_red[kThreads / 64][MEAS == kMeasSites ? kMaxObs : 2];
+
+  const int t = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y;
+  const int64_t g = A.batch_start + b;
+  const int inst = (int)(g / A.n_traj);
+  const uint64_t traj = (uint64_t)(A.traj_offset + (g % A.n_traj));
+
+  // sites handled by this pass: tile bits [c, 12) -> sites s + (k - c)
+  int act = 0;
+  for (int k = A.c; k < kTileBits; ++k)
+    if (A.s + (k - A.c) < A.L_real) act |= 1 << k;
+
+  if (t < kTileBits) {
+    double2 m[4];
+    if (act & (1 << t)) {
+      build_site_kick(A, A.s + (t - A.c), traj, m);
+    } else {
+      m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
+      m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
+    }
+    s_mat[t][0] = m[0]; s_mat[t][1] = m[1]; s_mat[t][2] = m[2]; s_mat[t][3] = m[3];
+  }
+  if (DIAG != kDiagNone) {
+    const double2* dt = A.diag + (int64_t)inst * A.n_chunks * 64;
+    for (int i = t; i < A.n_chunks * 64; i += kThreads) {
+      double2 e = dt[i];
+      if (DIAG == kDiagBeforeConj) e.y = -e.y;
+      s_diag[i] = e;
+    }
+  }
+
+  // tile base: tile-id bits deposited at [c, s) and [s + a, L_eff)
+  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
+  const int64_t tbase = (((int64_t)tile & mid_mask) << A.c) |
+                        (((int64_t)tile >> A.tile_bits_mid) << (A.s + A.a));
+  const int cmask = (1 << A.c) - 1;
+  const int c = A.c, s = A.s;
+  auto gidx = [&](int y) -> int64_t {
+    return tbase | (int64_t)(y & cmask) | ((int64_t)(y >> c) << s);
+  };
+
+  const double2* src = A.src + (int64_t)b * A.state_len;
+  double2 v[kRegs];
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) v[r] = src[gidx(tile_y(2, t, r))];
+
+  __syncthreads();  // s_mat, s_diag ready
+
+  if (DIAG == kDiagBeforeConj) {
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r)
+      v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(2, t, r))));
+  }
+
+  apply_nibble<2>(v, s_mat, act);
+  int layout = 2;
+  if (act & 0x0F0) {
+    if (act & 0x00F) {
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(0, t, r))];
+      apply_nibble<0>(v, s_mat, act);
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(0, t, r))] = v[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(1, t, r))];
+    apply_nibble<1>(v, s_mat, act);
+    layout = 1;
+  } else if (act & 0x00F) {
+    // only low sites active (tiny L padded to 12 bits)
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(0, t, r))];
+    apply_nibble<0>(v, s_mat, act);
+    layout = 0;
+  }
+
+  if (DIAG == kDiagAfter) {
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r)
+      v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(layout, t, r))));
+  }
+
+  if (MEAS != kMeasNone) {
+    const int wave = t >> 6, lane = t & 63;
+    double pr[kRegs];
+    double ptot = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
+      ptot += pr[r];
+    }
+    double tot = wave_sum(ptot);
+    if (lane == 0) s_red[wave][0] = tot;
+    if (MEAS == kMeasProbe) {
+      double z = 0.0;
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        const int64_t x = gidx(tile_y(layout, t, r));
+        z += ((x >> A.probe) & 1) ? -pr[r] : pr[r];
+      }
+      z = wave_sum(z);
+      if (lane == 0) s_red[wave][1] = z;
+    } else {
+      for (int i = 0; i < A.L_real; ++i) {
+        double z = 0.0;
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+          const int64_t x = gidx(tile_y(layout, t, r));
+          z += ((x >> i) & 1) ? -pr[r] : pr[r];
+        }
+        z = wave_sum(z);
+        if (lane == 0) s_red[wave][1 + i] = z;
+      }
+    }
+    __syncthreads();
+    if (t < A.n_obs) {
+      double acc = 0.0;
+      for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
+      A.partial[((int64_t)b * gridDim.x + tile) * A.n_obs + t] = acc;
+    }
+  }
+
+  double2* dst = A.dst + (int64_t)b * A.state_len;
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) dst[gidx(tile_y(layout, t, r))] = v[r];
+}
+
+hipError_t launch_pass(const PassArgs& a, int batch, int diag_mode, int meas_mode,
+                       hipStream_t stream) {
+  const int n_tiles = 1 << (a.L_eff - kTileBits);
+  dim3 grid(n_tiles, batch), block(kThreads);
+#define DTC_LAUNCH(D, M) hipLaunchKernelGGL((pass_kernel<D, M>), grid, block, 0, stream, a)
+  switch (diag_mode * 3 + meas_mode) {
+    case 0: DTC_LAUNCH(kDiagNone, kMeasNone); break;
+    case 1: DTC_LAUNCH(kDiagNone, kMeasProbe); break;
+    case 2: DTC_LAUNCH(kDiagNone, kMeasSites); break;
+    case 3: DTC_LAUNCH(kDiagAfter, kMeasNone); break;
+    case 4: DTC_LAUNCH(kDiagAfter, kMeasProbe); break;
+    case 5: DTC_LAUNCH(kDiagAfter, kMeasSites); break;
+    case 6: DTC_LAUNCH(kDiagBeforeConj, kMeasNone); break;
+    case 7: DTC_LAUNCH(kDiagBeforeConj, kMeasProbe); break;
+    case 8: DTC_LAUNCH(kDiagBeforeConj, kMeasSites); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef DTC_LAUNCH
+  return hipGetLastError();
+}
+
+__global__ void reduce_kernel(const double* __restrict__ partial, int n_tiles, int n_obs,
+                              int batch, double* __restrict__ out, int64_t out_stride) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch * n_obs) return;
+  const int b = i / n_obs, o = i - b * n_obs;
+  const double* p = partial + (int64_t)b * n_tiles * n_obs + o;
+  double acc = 0.0;
+  for (int k = 0; k < n_tiles; ++k) acc += p[(int64_t)k * n_obs];
+  out[(int64_t)b * out_stride + o] = acc;
+}
+
+hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
+                         double* out, int64_t out_stride, hipStream_t stream) {
+  const int n = batch * n_obs;
+  hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, partial,
+                     n_tiles, n_obs, batch, out, out_stride);
+  return hipGetLastError();
+}
+
+__global__ void set_basis_kernel(double2* state, int64_t state_len, const int64_t* idx,
+                                 int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  state[(int64_t)b * state_len + idx[b]] = make_double2(1.0, 0.0);
+}
+
+hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx, int batch,
+                            hipStream_t stream) {
+  hipLaunchKernelGGL(set_basis_kernel, dim3((batch + 63) / 64), dim3(64), 0, stream, state,
+                     state_len, idx, batch);
+  return hipGetLastError();
+}
+
+}  // namespace dtc

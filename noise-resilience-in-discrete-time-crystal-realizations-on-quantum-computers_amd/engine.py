@@ -1,0 +1,215 @@
+"""Host-side handle on the HIP engine (one ``dtc_ctx`` per device).
+
+This is the layer the reference's drivers reach through
+``AerSimulator(...).run(circ, shots).result().get_counts()`` (fast.py:156,
+211-212); here the whole t-sweep of a disorder instance is one call, see
+``include/dtc.h``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _capi
+from .kicks import kick_table, n_sub_of
+
+N_ANCILLA_NOISY_GATES = 6  # H, CZ=u2.cx.u2 (x2), H on the ancilla -> six noisy u2
+
+
+@dataclass
+class SweepSpec:
+    """Everything that defines one autocorrelator sweep (fast.py argparse +
+    disorder).  ``hs``: [n_inst][L], ``phis``: [n_inst][L-1]."""
+
+    L: int
+    T: int
+    hs: np.ndarray
+    phis: np.ndarray
+    g: float | list = 0.97
+    polarization: str = "x"
+    circular_frequency: float = 1.0
+    initial_state: str = "vacuum"
+    noise_prob: float = 0.05
+    use_noise: int = 1
+    t_offset: int = 0
+    probe_site: int | None = None
+    kick: np.ndarray | None = field(default=None, repr=False)
+
+    def __post_init__(self):
+        self.hs = np.ascontiguousarray(np.atleast_2d(self.hs)[:, : self.L], dtype=np.float64)
+        ph = np.atleast_2d(self.phis)
+        self.phis = np.ascontiguousarray(ph[:, : max(self.L - 1, 0)], dtype=np.float64)
+        if self.L == 1:
+            self.phis = np.zeros((self.hs.shape[0], 1))
+        if self.probe_site is None:
+            self.probe_site = int(self.L / 2)  # fast.py:221
+        if self.kick is None:
+            self.kick = kick_table(self.L, self.n_periods, self.g, self.polarization,
+                                   self.circular_frequency)
+        self.kick = np.ascontiguousarray(self.kick, dtype=np.float64)
+
+    @property
+    def n_inst(self) -> int:
+        return self.hs.shape[0]
+
+    @property
+    def n_periods(self) -> int:
+        return max(1, self.T - 1 + self.t_offset)
+
+    @property
+    def n_sub(self) -> int:
+        return self.kick.shape[2]
+
+    @property
+    def p(self) -> float:
+        return float(self.noise_prob) if self.use_noise else 0.0
+
+    @property
+    def init_mask(self) -> int:
+        return init_mask(self.L, self.initial_state)
+
+
+def init_mask(L: int, initial_state: str) -> int:
+    """fast.py:127-130: ``neel`` = X on circuit qubits 2, 4, ... (sites 1, 3, ...)."""
+    if initial_state == "vacuum":
+        return 0
+    if initial_state == "neel":
+        m = 0
+        for q in range(1, L + 1):
+            if q % 2 == 0:
+                m |= 1 << (q - 1)
+        return m
+    raise ValueError(f"initial_state must be 'vacuum' or 'neel', got {initial_state!r}")
+
+
+class DtcEngine:
+    """Owns one device context of libdtc_hip.so."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _capi.load_library()
+        ctx = ctypes.c_void_p()
+        _capi.check(self._lib.dtc_open(int(device), ctypes.byref(ctx)))
+        self._ctx = ctx
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._lib.dtc_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- structs -------------------------------------------------------
+    @staticmethod
+    def _problem(spec: SweepSpec, want_fwd=True, want_echo=True, batch=0):
+        pr = _capi.DtcProblem()
+        pr.L = spec.L
+        pr.T = spec.T
+        pr.n_inst = spec.n_inst
+        pr.probe_site = spec.probe_site
+        pr.t_offset = spec.t_offset
+        pr.n_sub = spec.n_sub
+        pr.init_mask = spec.init_mask
+        pr.h = _capi.as_dptr(spec.hs)
+        pr.phi = _capi.as_dptr(spec.phis)
+        pr.kick = _capi.as_dptr(spec.kick)
+        pr.want_fwd = int(bool(want_fwd))
+        pr.want_echo = int(bool(want_echo))
+        pr.batch = int(batch)
+        return pr
+
+    @staticmethod
+    def _noise(spec: SweepSpec):
+        nz = _capi.DtcNoise()
+        nz.p = spec.p
+        nz.n_anc = N_ANCILLA_NOISY_GATES
+        return nz
+
+    # -- API -------------------------------------------------------------
+    def autocorr(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
+                 traj_offset: int = 0, want_fwd: bool = True, want_echo: bool = True,
+                 want_zsite: bool = False, batch: int = 0):
+        """Per-trajectory ancilla expectations.
+
+        Returns dict with ``fwd``/``echo`` of shape [n_inst][n_traj][T] and
+        optionally ``zsite`` [n_inst][n_traj][T][L] (forward <Z_i>(t)).
+        """
+        n_inst, T, L = spec.n_inst, spec.T, spec.L
+        fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
+        echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
+        zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
+        pr = self._problem(spec, want_fwd, want_echo, batch)
+        nz = self._noise(spec)
+        _capi.check(self._lib.dtc_autocorr(
+            self._ctx, ctypes.byref(pr), ctypes.byref(nz), ctypes.c_uint64(seed),
+            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(fwd),
+            _capi.as_dptr(echo), _capi.as_dptr(zs)))
+        out = {}
+        if want_fwd:
+            out["fwd"] = fwd
+        if want_echo:
+            out["echo"] = echo
+        if want_zsite:
+            out["zsite"] = zs
+        return out
+
+    def apply_periods(self, spec: SweepSpec, state: np.ndarray, first_period: int,
+                      n_periods: int, inverse: bool = False, inst: int = 0, traj: int = 0,
+                      stream: int = 0, seed: int = 0x5EED0001):
+        """Apply periods to a host statevector (complex128 [2^L]); returns
+        ``(new_state, [norm, <Z_0>, ..., <Z_{L-1}>])``."""
+        psi = np.ascontiguousarray(state, dtype=np.complex128).copy()
+        if psi.shape != (1 << spec.L,):
+            raise ValueError("state must have 2^L amplitudes")
+        buf = psi.view(np.float64)
+        z = np.zeros(1 + spec.L)
+        pr = self._problem(spec)
+        nz = self._noise(spec)
+        _capi.check(self._lib.dtc_apply_periods(
+            self._ctx, ctypes.byref(pr), ctypes.byref(nz), ctypes.c_uint64(seed),
+            ctypes.c_int32(inst), ctypes.c_int64(traj), ctypes.c_uint32(stream),
+            ctypes.c_int32(first_period), ctypes.c_int32(n_periods),
+            ctypes.c_int32(int(inverse)), _capi.as_dptr(buf), _capi.as_dptr(z)))
+        return psi, z
+
+    # -- profiling -------------------------------------------------------
+    def set_profiling(self, on: bool):
+        _capi.check(self._lib.dtc_set_profiling(self._ctx, int(on)))
+
+    def reset_stats(self):
+        _capi.check(self._lib.dtc_reset_stats(self._ctx))
+
+    def kernel_stats(self):
+        out = {}
+        for k in range(4):
+            n = ctypes.c_int64()
+            ms = ctypes.c_double()
+            by = ctypes.c_double()
+            _capi.check(self._lib.dtc_kernel_stats(self._ctx, k, ctypes.byref(n),
+                                                   ctypes.byref(ms), ctypes.byref(by)))
+            out[k] = {"launches": n.value, "total_ms": ms.value, "bytes": by.value}
+        return out
+
+    def device_info(self):
+        name = ctypes.create_string_buffer(256)
+        ncu = ctypes.c_int32()
+        mem = ctypes.c_double()
+        _capi.check(self._lib.dtc_device_info(self._ctx, name, 256, ctypes.byref(ncu),
+                                              ctypes.byref(mem)))
+        return {"name": name.value.decode(), "n_cu": ncu.value, "hbm_bytes": mem.value}
+
+
+def spec_n_sub(polarization: str) -> int:
+    return n_sub_of(polarization)

@@ -1,0 +1,112 @@
+"""ctypes wrapper of oracle/liboracle.so (the C restatement in dtc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — used by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+class OrcProblem(ctypes.Structure):
+    _fields_ = [
+        ("L", ctypes.c_int32), ("T", ctypes.c_int32), ("n_inst", ctypes.c_int32),
+        ("probe_site", ctypes.c_int32), ("t_offset", ctypes.c_int32),
+        ("n_sub", ctypes.c_int32), ("init_mask", ctypes.c_uint64), ("h", _dp),
+        ("phi", _dp), ("kick", _dp), ("want_fwd", ctypes.c_int32),
+        ("want_echo", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class OrcNoise(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_double), ("n_anc", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle not built: {LIB_PATH} (run `make`)")
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.orc_autocorr.argtypes = [ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcNoise),
+                                      ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, _dp, _dp,
+                                      _dp, ctypes.c_int32]
+        _lib.orc_apply_periods.argtypes = [ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcNoise),
+                                           ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64,
+                                           ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, _dp, _dp]
+        _lib.orc_sample_pauli.argtypes = [ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32]
+        _lib.orc_sample_pauli.restype = ctypes.c_int
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def _problem(spec, want_fwd=True, want_echo=True):
+    pr = OrcProblem()
+    pr.L, pr.T, pr.n_inst = spec.L, spec.T, spec.n_inst
+    pr.probe_site, pr.t_offset, pr.n_sub = spec.probe_site, spec.t_offset, spec.n_sub
+    pr.init_mask = spec.init_mask
+    pr.h, pr.phi, pr.kick = _ptr(spec.hs), _ptr(spec.phis), _ptr(spec.kick)
+    pr.want_fwd, pr.want_echo = int(want_fwd), int(want_echo)
+    return pr
+
+
+def _noise(spec, n_anc=6):
+    nz = OrcNoise()
+    nz.p = spec.p
+    nz.n_anc = n_anc
+    return nz
+
+
+def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_echo=True,
+             want_zsite=False, n_threads=0):
+    """Same contract as DtcEngine.autocorr (per-trajectory outputs)."""
+    n_inst, T, L = spec.n_inst, spec.T, spec.L
+    fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
+    echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
+    zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
+    rc = lib().orc_autocorr(ctypes.byref(_problem(spec, want_fwd, want_echo)),
+                            ctypes.byref(_noise(spec)), seed, traj_offset, n_traj, _ptr(fwd),
+                            _ptr(echo), _ptr(zs), n_threads)
+    if rc != 0:
+        raise RuntimeError(f"orc_autocorr failed: {rc}")
+    out = {}
+    if want_fwd:
+        out["fwd"] = fwd
+    if want_echo:
+        out["echo"] = echo
+    if want_zsite:
+        out["zsite"] = zs
+    return out
+
+
+def apply_periods(spec, state, first_period, n_periods, inverse=False, inst=0, traj=0,
+                  stream=0, seed=0x5EED0001):
+    psi = np.ascontiguousarray(state, dtype=np.complex128).copy()
+    z = np.zeros(1 + spec.L)
+    lib().orc_apply_periods(ctypes.byref(_problem(spec)), ctypes.byref(_noise(spec)), seed, inst,
+                            traj, stream, first_period, n_periods, int(inverse),
+                            _ptr(psi.view(np.float64)), _ptr(z))
+    return psi, z
+
+
+def sample_pauli(p, seed, traj, stream, period, site, sub):
+    return lib().orc_sample_pauli(p, seed, traj, stream, period, site, sub)
