@@ -81,7 +81,7 @@ int ensure(DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.n >= bytes) return DTC_OK;
   if (b.p) {
-    hipFree(b.p);
+    (void)hipFree(b.p);
     b.p = nullptr;
     b.n = 0;
   }
@@ -91,7 +91,7 @@ int ensure(DevBuf& b, size_t bytes) {
 }
 
 void release(DevBuf& b) {
-  if (b.p) hipFree(b.p);
+  if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.n = 0;
 }
@@ -103,7 +103,7 @@ hipEvent_t get_event(dtc_ctx* ctx) {
     return e;
   }
   hipEvent_t e = nullptr;
-  hipEventCreate(&e);
+  (void)hipEventCreate(&e);
   return e;
 }
 
@@ -149,32 +149,46 @@ Plan make_plan(int L) {
 }
 
 // Diagonal factor tables (RZZ even/odd bonds + RZ, fast.py:115-120):
-// D(x) = exp(-i/2 (sum_i h_i z_i + sum_i phi_i z_i z_{i+1})), z_i = 1 - 2 bit_i(x),
-// factored as prod_k T_k[(x >> 5k) & 63]; T_k covers sites 5k..5k+4 and the bond
-// to site 5k+5 (index bit 5).
+// D(x) = exp(-i/2 (sum_i h_i z_i + sum_i phi_i z_i z_{i+1})), z_i = 1 - 2 bit_i(x).
+// Per instance: n_chunks chunk tables, D(x) = prod_k C_k[(x >> 5k) & 63] (C_k covers
+// sites 5k..5k+4 and the bond to site 5k+5 = index bit 5), followed by 3 register-
+// nibble tables N_n[v], v = bits [4n-1, 4n+5) of x, holding the terms of sites
+// 4n..4n+3 and of the bonds touching them (the kernel's apply_diag_nibble<n>).
+double diag_angle(int L, const double* hh, const double* pp, int lo_site, int hi_site,
+                  int bond_lo, int bond_hi, int bit0, int v) {
+  auto z = [&](int i) -> double { return ((v >> (i - bit0)) & 1) ? -1.0 : 1.0; };
+  double ang = 0.0;
+  for (int i = lo_site; i < hi_site && i < L; ++i) ang += hh[i] * z(i);
+  for (int i = std::max(bond_lo, 0); i < bond_hi && i + 1 < L; ++i) ang += pp[i] * z(i) * z(i + 1);
+  return ang;
+}
+
 void build_diag_tables(const Plan& pl, int n_inst, const double* h, const double* phi,
                        std::vector<double>& out) {
   const int L = pl.L;
-  out.assign((size_t)n_inst * pl.n_chunks * 64 * 2, 0.0);
+  const int per_inst = (pl.n_chunks + 3) * 64;
+  out.assign((size_t)n_inst * per_inst * 2, 0.0);
   for (int in = 0; in < n_inst; ++in) {
     const double* hh = h + (size_t)in * L;
     const double* pp = phi + (size_t)in * (L > 1 ? L - 1 : 0);
+    double* o = out.data() + (size_t)in * per_inst * 2;
     for (int k = 0; k < pl.n_chunks; ++k) {
+      const int b0 = dtc::kChunkBits * k;
       for (int v = 0; v < 64; ++v) {
-        double ang = 0.0;
-        for (int q = 0; q < dtc::kChunkBits; ++q) {
-          const int i = dtc::kChunkBits * k + q;
-          if (i >= L) break;
-          const double zi = ((v >> q) & 1) ? -1.0 : 1.0;
-          ang += hh[i] * zi;
-          if (i + 1 < L) {
-            const double zj = ((v >> (q + 1)) & 1) ? -1.0 : 1.0;
-            ang += pp[i] * zi * zj;
-          }
-        }
-        const size_t o = (((size_t)in * pl.n_chunks + k) * 64 + v) * 2;
-        out[o] = std::cos(-0.5 * ang);
-        out[o + 1] = std::sin(-0.5 * ang);
+        const double ang = diag_angle(L, hh, pp, b0, b0 + dtc::kChunkBits, b0,
+                                      b0 + dtc::kChunkBits, b0, v);
+        o[(k * 64 + v) * 2] = std::cos(-0.5 * ang);
+        o[(k * 64 + v) * 2 + 1] = std::sin(-0.5 * ang);
+      }
+    }
+    for (int n = 0; n < 3; ++n) {
+      const int b0 = 4 * n - 1;
+      for (int v = 0; v < 64; ++v) {
+        if (n == 0 && (v & 1)) continue;  // bit -1 does not exist
+        const double ang = diag_angle(L, hh, pp, 4 * n, 4 * n + 4, 4 * n - 1, 4 * n + 4, b0, v);
+        const int e = (pl.n_chunks + n) * 64 + v;
+        o[e * 2] = std::cos(-0.5 * ang);
+        o[e * 2 + 1] = std::sin(-0.5 * ang);
       }
     }
   }
@@ -393,13 +407,13 @@ int dtc_open(int32_t device, dtc_ctx** out) {
 
 int dtc_close(dtc_ctx* ctx) {
   if (!ctx) return DTC_OK;
-  hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
   for (auto& p : ctx->pending) {
-    hipEventDestroy(p.e0);
-    hipEventDestroy(p.e1);
+    (void)hipEventDestroy(p.e0);
+    (void)hipEventDestroy(p.e1);
   }
-  for (auto e : ctx->pool) hipEventDestroy(e);
+  for (auto e : ctx->pool) (void)hipEventDestroy(e);
   release(ctx->F);
   release(ctx->E);
   release(ctx->partial);
@@ -408,7 +422,7 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->diag);
   release(ctx->kick);
   release(ctx->basis);
-  hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return DTC_OK;
 }

@@ -133,6 +133,29 @@ __device__ __forceinline__ double2 diag_phase(const double2* s_diag, int n_chunk
   return ph;
 }
 
+// Index of the register-nibble table N: bits [4N-1, 4N+5) of x (bit -1 = 0).
+__device__ __forceinline__ int nib_index(int64_t x, int N) {
+  return (int)(((x << 1) >> (4 * N)) & 63);
+}
+
+// Diagonal on the 16 amplitudes of a thread whose registers span global bits
+// [4N, 4N+4) (low pass: tile bits == global bits).  D(x) = P_C * T_N[x], with
+// the thread constant P_C = D(x0) / T_N[x0] computed once: one LDS lookup and
+// two complex products per amplitude instead of n_chunks lookups.
+template <int N>
+__device__ __forceinline__ void apply_diag_nibble(double2 (&v)[kRegs], const double2* s_diag,
+                                                  int n_chunks, int64_t x0) {
+  const double2* tn = s_diag + (n_chunks + N) * 64;
+  const double2 d0 = diag_phase(s_diag, n_chunks, x0);
+  const double2 r0 = tn[nib_index(x0, N)];
+  const double2 pc = cmul(d0, make_double2(r0.x, -r0.y));
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    const int64_t x = x0 | ((int64_t)r << (4 * N));
+    v[r] = cmul(v[r], cmul(pc, tn[nib_index(x, N)]));
+  }
+}
+
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
@@ -140,9 +163,9 @@ __device__ __forceinline__ double wave_sum(double x) {
 }
 
 template <int DIAG, int MEAS>
-__global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
+__device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double2 s_tile[kTile];
-  __shared__ double2 s_diag[DIAG != kDiagNone ? kMaxChunks * 64 : 1];
+  __shared__ double2 s_diag[DIAG != kDiagNone ? (kMaxChunks + 3) * 64 : 1];
   __shared__ double2 s_mat[kTileBits][4];
   __shared__ double s_red[kThreads / 64][MEAS == kMeasSites ? kMaxObs : 2];
 
@@ -169,8 +192,9 @@ __global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
     s_mat[t][0] = m[0]; s_mat[t][1] = m[1]; s_mat[t][2] = m[2]; s_mat[t][3] = m[3];
   }
   if (DIAG != kDiagNone) {
-    const double2* dt = A.diag + (int64_t)inst * A.n_chunks * 64;
-    for (int i = t; i < A.n_chunks * 64; i += kThreads) {
+    const int n_tab = (A.n_chunks + 3) * 64;
+    const double2* dt = A.diag + (int64_t)inst * n_tab;
+    for (int i = t; i < n_tab; i += kThreads) {
       double2 e = dt[i];
       if (DIAG == kDiagBeforeConj) e.y = -e.y;
       s_diag[i] = e;
@@ -194,11 +218,7 @@ __global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
 
   __syncthreads();  // s_mat, s_diag ready
 
-  if (DIAG == kDiagBeforeConj) {
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r)
-      v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(2, t, r))));
-  }
+  if (DIAG == kDiagBeforeConj) apply_diag_nibble<2>(v, s_diag, A.n_chunks, gidx(tile_y(2, t, 0)));
 
   apply_nibble<2>(v, s_mat, act);
   int layout = 2;
@@ -234,9 +254,13 @@ __global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
   }
 
   if (DIAG == kDiagAfter) {
+    if (layout == 1) {
+      apply_diag_nibble<1>(v, s_diag, A.n_chunks, gidx(tile_y(1, t, 0)));
+    } else {
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r)
-      v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(layout, t, r))));
+      for (int r = 0; r < kRegs; ++r)
+        v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(layout, t, r))));
+    }
   }
 
   if (MEAS != kMeasNone) {
@@ -284,21 +308,35 @@ __global__ __launch_bounds__(kThreads, 2) void pass_kernel(PassArgs A) {
   for (int r = 0; r < kRegs; ++r) dst[gidx(tile_y(layout, t, r))] = v[r];
 }
 
+// Distinct kernel symbols per pass kind so rocprofv3 traces separate them.
+template <int MEAS>
+__global__ __launch_bounds__(kThreads, 2) void dtc_hi_pass(PassArgs A) {
+  pass_body<kDiagNone, MEAS>(A);
+}
+template <int MEAS>
+__global__ __launch_bounds__(kThreads, 2) void dtc_lo_pass_fwd(PassArgs A) {
+  pass_body<kDiagAfter, MEAS>(A);
+}
+template <int MEAS>
+__global__ __launch_bounds__(kThreads, 2) void dtc_lo_pass_inv(PassArgs A) {
+  pass_body<kDiagBeforeConj, MEAS>(A);
+}
+
 hipError_t launch_pass(const PassArgs& a, int batch, int diag_mode, int meas_mode,
                        hipStream_t stream) {
   const int n_tiles = 1 << (a.L_eff - kTileBits);
   dim3 grid(n_tiles, batch), block(kThreads);
-#define DTC_LAUNCH(D, M) hipLaunchKernelGGL((pass_kernel<D, M>), grid, block, 0, stream, a)
+#define DTC_LAUNCH(K, M) hipLaunchKernelGGL((K<M>), grid, block, 0, stream, a)
   switch (diag_mode * 3 + meas_mode) {
-    case 0: DTC_LAUNCH(kDiagNone, kMeasNone); break;
-    case 1: DTC_LAUNCH(kDiagNone, kMeasProbe); break;
-    case 2: DTC_LAUNCH(kDiagNone, kMeasSites); break;
-    case 3: DTC_LAUNCH(kDiagAfter, kMeasNone); break;
-    case 4: DTC_LAUNCH(kDiagAfter, kMeasProbe); break;
-    case 5: DTC_LAUNCH(kDiagAfter, kMeasSites); break;
-    case 6: DTC_LAUNCH(kDiagBeforeConj, kMeasNone); break;
-    case 7: DTC_LAUNCH(kDiagBeforeConj, kMeasProbe); break;
-    case 8: DTC_LAUNCH(kDiagBeforeConj, kMeasSites); break;
+    case 0: DTC_LAUNCH(dtc_hi_pass, kMeasNone); break;
+    case 1: DTC_LAUNCH(dtc_hi_pass, kMeasProbe); break;
+    case 2: DTC_LAUNCH(dtc_hi_pass, kMeasSites); break;
+    case 3: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasNone); break;
+    case 4: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasProbe); break;
+    case 5: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasSites); break;
+    case 6: DTC_LAUNCH(dtc_lo_pass_inv, kMeasNone); break;
+    case 7: DTC_LAUNCH(dtc_lo_pass_inv, kMeasProbe); break;
+    case 8: DTC_LAUNCH(dtc_lo_pass_inv, kMeasSites); break;
     default: return hipErrorInvalidValue;
   }
 #undef DTC_LAUNCH
