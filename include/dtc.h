@@ -76,7 +76,8 @@ typedef struct dtc_problem {
   int32_t want_fwd;    /* compute the forward autocorrelator              */
   int32_t want_echo;   /* compute the echo autocorrelator                 */
   int32_t batch;       /* states per device batch, 0 = automatic          */
-  int32_t reserved;
+  int32_t t_first;     /* outputs for t < t_first are skipped (left as 0):
+                          a single-circuit call (one t) sets t_first = T-1 */
 } dtc_problem;
 
 /* Noise model (fast.py:76-86): depolarizing_error(p, 1) after every noisy

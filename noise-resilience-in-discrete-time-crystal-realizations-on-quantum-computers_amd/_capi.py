@@ -60,7 +60,7 @@ class DtcProblem(ctypes.Structure):
         ("want_fwd", ctypes.c_int32),
         ("want_echo", ctypes.c_int32),
         ("batch", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("t_first", ctypes.c_int32),
     ]
 
 

@@ -326,6 +326,7 @@ int check_problem(const dtc_problem* pr, const dtc_noise* nz) {
   if (pr->probe_site < 0 || pr->probe_site >= pr->L)
     return fail(DTC_EINVAL, "probe_site out of range");
   if (pr->t_offset < 0) return fail(DTC_EINVAL, "t_offset must be >= 0");
+  if (pr->t_first < 0 || pr->t_first >= pr->T) return fail(DTC_EINVAL, "t_first out of range");
   if (pr->n_sub < 1 || pr->n_sub > 8) return fail(DTC_EINVAL, "n_sub must be in [1, 8]");
   if (!pr->h || (!pr->phi && pr->L > 1) || !pr->kick)
     return fail(DTC_EINVAL, "null h/phi/kick");
@@ -545,13 +546,13 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
     for (int p = 0; p <= P; ++p) {
       const int t = p - pr->t_offset;
       if (p > 0) {
-        const bool meas = want_f && t >= 0;
+        const bool meas = want_f && t >= 0 && t >= pr->t_first;
         DTC_TRY(forward_period(ctx, rc, bs, nb, F, F, p, dtc::kStreamForward,
                                meas ? meas_f : dtc::kMeasNone, n_obs_f,
                                meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
                                (int64_t)T * n_obs_f));
       }
-      if (t < 0 || !want_e || p == 0) continue;
+      if (t < 0 || t < pr->t_first || !want_e || p == 0) continue;
       double* vout = (double*)ctx->vals_e.p + (size_t)t * 2;
       for (int k = 1; k <= p; ++k) {
         const bool last = (k == p);
@@ -573,7 +574,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
       const int64_t g = bs + b;
       const uint64_t m = (uint64_t)masks[b];
       const double zinit = ((m >> j) & 1ull) ? -1.0 : 1.0;
-      for (int t = 0; t < T; ++t) {
+      for (int t = std::max(0, pr->t_first); t < T; ++t) {
         const bool at_init = (t + pr->t_offset == 0);
         const double* vf = hv_f.data() + ((size_t)b * T + t) * n_obs_f;
         const double zj_f = at_init ? zinit : (want_z ? vf[1 + j] : vf[1]);

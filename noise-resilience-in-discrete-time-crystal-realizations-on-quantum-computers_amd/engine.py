@@ -36,6 +36,7 @@ class SweepSpec:
     t_offset: int = 0
     probe_site: int | None = None
     kick: np.ndarray | None = field(default=None, repr=False)
+    init_mask_value: int | None = None   # explicit Z-basis prep (overrides initial_state)
 
     def __post_init__(self):
         self.hs = np.ascontiguousarray(np.atleast_2d(self.hs)[:, : self.L], dtype=np.float64)
@@ -68,6 +69,8 @@ class SweepSpec:
 
     @property
     def init_mask(self) -> int:
+        if self.init_mask_value is not None:
+            return int(self.init_mask_value)
         return init_mask(self.L, self.initial_state)
 
 
@@ -113,7 +116,7 @@ class DtcEngine:
 
     # -- structs -------------------------------------------------------
     @staticmethod
-    def _problem(spec: SweepSpec, want_fwd=True, want_echo=True, batch=0):
+    def _problem(spec: SweepSpec, want_fwd=True, want_echo=True, batch=0, t_first=0):
         pr = _capi.DtcProblem()
         pr.L = spec.L
         pr.T = spec.T
@@ -128,6 +131,7 @@ class DtcEngine:
         pr.want_fwd = int(bool(want_fwd))
         pr.want_echo = int(bool(want_echo))
         pr.batch = int(batch)
+        pr.t_first = int(t_first)
         return pr
 
     @staticmethod
@@ -140,7 +144,7 @@ class DtcEngine:
     # -- API -------------------------------------------------------------
     def autocorr(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
                  traj_offset: int = 0, want_fwd: bool = True, want_echo: bool = True,
-                 want_zsite: bool = False, batch: int = 0):
+                 want_zsite: bool = False, batch: int = 0, t_first: int = 0):
         """Per-trajectory ancilla expectations.
 
         Returns dict with ``fwd``/``echo`` of shape [n_inst][n_traj][T] and
@@ -150,7 +154,7 @@ class DtcEngine:
         fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
         echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
         zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
-        pr = self._problem(spec, want_fwd, want_echo, batch)
+        pr = self._problem(spec, want_fwd, want_echo, batch, t_first)
         nz = self._noise(spec)
         _capi.check(self._lib.dtc_autocorr(
             self._ctx, ctypes.byref(pr), ctypes.byref(nz), ctypes.c_uint64(seed),

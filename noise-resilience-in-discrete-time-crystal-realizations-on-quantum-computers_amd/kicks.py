@@ -41,29 +41,36 @@ def ry(theta: float) -> np.ndarray:
     return np.array([[c, -s], [s, c]], dtype=np.complex128)
 
 
-def period_gates(polarization: str, g: float, step: int, circular_frequency: float = 1.0):
-    """Sub-gate list (application order) of one site's kick at period index ``step``."""
+def period_gate_specs(polarization: str, g: float, step: int, circular_frequency: float = 1.0):
+    """Sub-gate list [(name, angle)] (application order) of one site's kick at
+    period index ``step`` (0-based)."""
     pg = math.pi * g
     if polarization == "x":
-        return [rx(pg)]
+        return [("rx", pg)]
     if polarization == "y":
-        return [ry(pg)]
+        return [("ry", pg)]
     if polarization == "xy":
-        return [rx(pg / 2), ry(pg / 2)]
+        return [("rx", pg / 2), ("ry", pg / 2)]
     if polarization == "yx":
-        return [ry(pg / 2), rx(pg / 2)]
+        return [("ry", pg / 2), ("rx", pg / 2)]
     if polarization in ("circular_left", "circular_right"):
         w = circular_frequency
         ax = pg * math.cos(w * step) / math.sqrt(2)
         ay = pg * math.sin(w * step) / math.sqrt(2)
         if polarization == "circular_right":
             ay = -ay
-        return [rx(ax), ry(ay)]
+        return [("rx", ax), ("ry", ay)]
     if polarization == "circular_static":
-        return [rx(pg / math.sqrt(2)), ry(pg / math.sqrt(2))]
+        return [("rx", pg / math.sqrt(2)), ("ry", pg / math.sqrt(2))]
     if polarization == "xy_cycle":
-        return [rx(pg)] if (step // 5) % 2 == 0 else [ry(pg)]
+        return [("rx", pg)] if (step // 5) % 2 == 0 else [("ry", pg)]
     raise ValueError(f"unknown polarization {polarization!r}; expected one of {POLARIZATIONS}")
+
+
+def period_gates(polarization: str, g: float, step: int, circular_frequency: float = 1.0):
+    """Sub-gate matrices (application order) of one site's kick at period ``step``."""
+    return [rx(a) if n == "rx" else ry(a)
+            for n, a in period_gate_specs(polarization, g, step, circular_frequency)]
 
 
 def kick_table(L: int, n_periods: int, g: float | Sequence[float] = 0.97,

@@ -23,7 +23,7 @@ class OrcProblem(ctypes.Structure):
         ("n_sub", ctypes.c_int32), ("init_mask", ctypes.c_uint64), ("h", _dp),
         ("phi", _dp), ("kick", _dp), ("want_fwd", ctypes.c_int32),
         ("want_echo", ctypes.c_int32), ("batch", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("t_first", ctypes.c_int32),
     ]
 
 
@@ -59,13 +59,14 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(_dp)
 
 
-def _problem(spec, want_fwd=True, want_echo=True):
+def _problem(spec, want_fwd=True, want_echo=True, t_first=0):
     pr = OrcProblem()
     pr.L, pr.T, pr.n_inst = spec.L, spec.T, spec.n_inst
     pr.probe_site, pr.t_offset, pr.n_sub = spec.probe_site, spec.t_offset, spec.n_sub
     pr.init_mask = spec.init_mask
     pr.h, pr.phi, pr.kick = _ptr(spec.hs), _ptr(spec.phis), _ptr(spec.kick)
     pr.want_fwd, pr.want_echo = int(want_fwd), int(want_echo)
+    pr.t_first = int(t_first)
     return pr
 
 
@@ -77,13 +78,13 @@ def _noise(spec, n_anc=6):
 
 
 def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_echo=True,
-             want_zsite=False, n_threads=0):
+             want_zsite=False, n_threads=0, t_first=0):
     """Same contract as DtcEngine.autocorr (per-trajectory outputs)."""
     n_inst, T, L = spec.n_inst, spec.T, spec.L
     fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
     echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
     zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
-    rc = lib().orc_autocorr(ctypes.byref(_problem(spec, want_fwd, want_echo)),
+    rc = lib().orc_autocorr(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
                             ctypes.byref(_noise(spec)), seed, traj_offset, n_traj, _ptr(fwd),
                             _ptr(echo), _ptr(zs), n_threads)
     if rc != 0:

@@ -50,7 +50,7 @@ typedef struct orc_problem {
   const double* h;
   const double* phi;
   const double* kick;
-  int32_t want_fwd, want_echo, batch, reserved;
+  int32_t want_fwd, want_echo, batch, t_first;
 } orc_problem;
 
 typedef struct orc_noise {
@@ -269,7 +269,7 @@ int orc_autocorr(const orc_problem* pr, const orc_noise* nz, uint64_t seed, int6
     for (int p = 0; p <= P; ++p) {
       const int t = p - pr->t_offset;
       if (p > 0) period_forward(pr, &rng, inst, F, p, traj, 0u);
-      if (t < 0) continue;
+      if (t < 0 || t < pr->t_first) continue;
       if (pr->want_fwd || zsite) {
         measure_z(F, L, z);
         if (pr->want_fwd) fwd[(size_t)g * T + t] = fac * zinit * z[1 + pr->probe_site];

@@ -1,0 +1,158 @@
+"""HIP engine (through the C ABI) vs the CPU oracle, per trajectory.
+
+The engine and oracle share the RNG contract of include/dtc.h, so each noisy
+trajectory is the same random circuit on both sides: per-trajectory
+autocorrelator values must agree to 1e-10 (summation order is the only
+difference; observed ~1e-13 at L=20).
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle, dm_oracle
+from tests.helpers import random_disorder
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def _cmp(a, b, tol=TOL):
+    for k in b:
+        err = float(np.abs(a[k] - b[k]).max())
+        assert err < tol, (k, err)
+
+
+CASES = [
+    # L, T, n_inst, n_traj, p, state, pol, t_offset
+    (4, 20, 1, 1, 0.0, "vacuum", "x", 0),
+    (4, 12, 1, 6, 0.05, "neel", "x", 0),
+    (5, 9, 2, 3, 0.1, "vacuum", "circular_left", 0),
+    (8, 9, 1, 4, 0.05, "neel", "yx", 1),
+    (11, 8, 1, 3, 0.05, "vacuum", "xy_cycle", 0),
+    (12, 8, 2, 3, 0.05, "vacuum", "x", 0),
+    (13, 7, 1, 3, 0.2, "neel", "y", 0),
+    (15, 6, 1, 2, 0.05, "vacuum", "xy", 1),
+    (16, 6, 1, 2, 0.05, "neel", "circular_right", 0),
+    (17, 5, 1, 2, 0.05, "vacuum", "x", 0),
+    (20, 6, 1, 2, 0.05, "vacuum", "x", 0),
+]
+
+
+@pytest.mark.parametrize("L,T,n_inst,n_traj,p,state,pol,toff", CASES)
+def test_engine_matches_oracle(pkg, engine, L, T, n_inst, n_traj, p, state, pol, toff):
+    rng = np.random.default_rng(L * 100 + T)
+    hs, phis = random_disorder(rng, L, n_inst)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    got = engine.autocorr(spec, n_traj, seed=1234, want_zsite=True)
+    ref = c_oracle.autocorr(spec, n_traj, seed=1234, want_zsite=True)
+    _cmp(got, ref)
+
+
+def test_per_period_g_list(pkg, engine):
+    """controlled-g.py: g_values[step] per period, t+1 periods."""
+    rng = np.random.default_rng(3)
+    L, T = 10, 8
+    hs, phis = random_disorder(rng, L)
+    gl = list(np.linspace(0.84, 1.0, T))
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=gl, noise_prob=0.05, t_offset=1)
+    _cmp(engine.autocorr(spec, 3, seed=5), c_oracle.autocorr(spec, 3, seed=5))
+
+
+@pytest.mark.parametrize("L", [4, 9, 12, 14, 18, 20])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_apply_periods_random_state(pkg, engine, L, inverse):
+    rng = np.random.default_rng(L + 7 * inverse)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=5, hs=hs, phis=phis, g=0.97, noise_prob=0.1, polarization="xy")
+    psi = rng.normal(size=1 << L) + 1j * rng.normal(size=1 << L)
+    psi /= np.linalg.norm(psi)
+    first = 3 if inverse else 2
+    ga, gz = engine.apply_periods(spec, psi, first, 3, inverse=inverse, inst=1, traj=11,
+                                  stream=4, seed=99)
+    oa, oz = c_oracle.apply_periods(spec, psi, first, 3, inverse=inverse, inst=1, traj=11,
+                                    stream=4, seed=99)
+    assert np.abs(ga - oa).max() < 1e-12
+    assert np.abs(gz - oz).max() < 1e-11
+
+
+def test_forward_inverse_roundtrip_noiseless(pkg, engine):
+    rng = np.random.default_rng(1)
+    L = 20
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=8, hs=hs, phis=phis, g=0.97, noise_prob=0.0, use_noise=0)
+    psi = rng.normal(size=1 << L) + 1j * rng.normal(size=1 << L)
+    psi /= np.linalg.norm(psi)
+    a, za = engine.apply_periods(spec, psi, 1, 7)
+    assert abs(za[0] - 1.0) < 1e-12
+    b, _ = engine.apply_periods(spec, a, 7, 7, inverse=True)
+    assert np.abs(b - psi).max() < 1e-12
+
+
+def test_noiseless_L20_statevector_oracle(pkg, engine, golden):
+    """hs_L20 row 0, g=0.97: forward <Z_i>(t) vs the numpy statevector oracle."""
+    d = golden["disorder"]["L20"]
+    hs, phis = np.array(d["hs"][:1]), np.array(d["phis"][:1])
+    spec = pkg.SweepSpec(L=20, T=10, hs=hs, phis=phis, g=0.97, noise_prob=0.0, use_noise=0)
+    out = engine.autocorr(spec, 1, want_zsite=True, want_echo=True)
+    z = dm_oracle.statevector_zsite(20, 10, hs[0], phis[0], spec.kick)
+    assert np.abs(out["zsite"][0, 0] - z).max() < 1e-10
+    np.testing.assert_allclose(out["fwd"][0, 0], z[:, 10], atol=1e-10)
+    # <Z_10(t)> for t = 0..3
+    np.testing.assert_allclose(z[:4, 10], [1, -0.995562, 0.999894, -0.994949], atol=1e-6)
+    np.testing.assert_allclose(out["echo"][0, 0], np.ones(10), atol=1e-10)
+
+
+def test_batching_and_sharding_invariance(pkg, engine):
+    """Per-trajectory values depend only on the global trajectory id."""
+    rng = np.random.default_rng(4)
+    L = 14
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=6, hs=hs, phis=phis, g=0.9, noise_prob=0.1)
+    full = engine.autocorr(spec, 6, seed=21, batch=0)
+    b1 = engine.autocorr(spec, 6, seed=21, batch=1)
+    b5 = engine.autocorr(spec, 6, seed=21, batch=5)
+    lo = engine.autocorr(spec, 2, seed=21, traj_offset=0)
+    hi = engine.autocorr(spec, 4, seed=21, traj_offset=2)
+    for k in ("fwd", "echo"):
+        assert np.array_equal(full[k], b1[k]) and np.array_equal(full[k], b5[k])
+        assert np.array_equal(full[k], np.concatenate([lo[k], hi[k]], axis=1))
+
+
+def test_t_first_single_time_point(pkg, engine):
+    rng = np.random.default_rng(6)
+    hs, phis = random_disorder(rng, 12)
+    spec = pkg.SweepSpec(L=12, T=7, hs=hs, phis=phis, noise_prob=0.05)
+    full = engine.autocorr(spec, 3, seed=8)
+    last = engine.autocorr(spec, 3, seed=8, t_first=6)
+    for k in ("fwd", "echo"):
+        assert np.array_equal(full[k][..., 6], last[k][..., 6])
+        assert not np.any(last[k][..., :6])
+
+
+def test_error_paths(pkg, engine):
+    rng = np.random.default_rng(0)
+    hs, phis = random_disorder(rng, 6)
+    spec = pkg.SweepSpec(L=6, T=4, hs=hs, phis=phis)
+    with pytest.raises(pkg._capi.DtcError, match="n_traj"):
+        engine.autocorr(spec, 0)
+    bad = pkg.SweepSpec(L=6, T=4, hs=hs, phis=phis, probe_site=6)
+    with pytest.raises(pkg._capi.DtcError, match="probe_site"):
+        engine.autocorr(bad, 1)
+    with pytest.raises(pkg._capi.DtcError, match="period range"):
+        engine.apply_periods(spec, np.eye(1, 64)[0], 3, 4)
+
+
+def test_distribution_statistics_L8(pkg, engine):
+    """Trajectory means vs the exact noisy density matrix (z-test)."""
+    rng = np.random.default_rng(12)
+    L, T, n = 8, 8, 4096
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.95, noise_prob=0.05,
+                         initial_state="neel")
+    out = engine.autocorr(spec, n, seed=2024)
+    f, e = dm_oracle.folded_sweep(L, T, hs[0], phis[0], spec.kick, 0.05, initial_state="neel")
+    for key, exact in (("fwd", f), ("echo", e)):
+        a = out[key][0]
+        sd = a.std(axis=0)
+        z = np.abs(a.mean(axis=0) - exact)[sd > 0] / (sd[sd > 0] / np.sqrt(n))
+        assert z.max() < 4.5, (key, z)
