@@ -9,6 +9,13 @@
 // so the forward sweep costs T-1+t_offset periods per trajectory instead of
 // sum_t t, and each echo point branches off the forward prefix (same
 // per-t marginal distribution as the reference's independent circuits).
+//
+// Both sweeps are "layer chains" X_0 D X_1 D ... (X = a layer of single-site
+// kicks, D = the RZZ/RZ diagonal or its conjugate).  The sites are split in
+// groups that fit a tile; the scheduler (next_pass) emits passes that each
+// finish the pending kick layer on one group, apply D if that completed the
+// layer on every group, and start the next layer on the same group.  With two
+// groups (L <= 21) every pass applies one D: one HBM round trip per period.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -51,8 +58,9 @@ struct DevBuf {
   size_t n = 0;
 };
 
-struct Geom {
-  int c, s, a;
+struct Group {
+  int c, s;  // tile = bits [0, c) + [s, s + 12 - c)
+  int act;   // active tile-bit mask
 };
 
 struct Pending {
@@ -123,12 +131,14 @@ int resolve_pending(dtc_ctx* ctx) {
 }
 
 struct Plan {
-  int L = 0, L_eff = 0, n_chunks = 0, n_tiles = 0;
+  int L = 0, L_eff = 0, n_chunks = 0, n_tiles = 0, diag_stride = 0;
   int64_t len = 0;
-  Geom lo{0, 0, dtc::kTileBits};
-  std::vector<Geom> hi;
+  std::vector<Group> groups;
 };
 
+// Site groups: group 0 = sites [0, a0) in a contiguous 4096-amplitude tile;
+// further groups take up to `hi_max` sites each (tile = 12 - a column bits of
+// >= 128-B rows + the group's sites).  Defaults: 11 + 9 for L = 20.
 Plan make_plan(int L) {
   Plan pl;
   pl.L = L;
@@ -136,12 +146,31 @@ Plan make_plan(int L) {
   pl.len = (int64_t)1 << pl.L_eff;
   pl.n_tiles = 1 << (pl.L_eff - dtc::kTileBits);
   pl.n_chunks = (pl.L_eff + dtc::kChunkBits - 1) / dtc::kChunkBits;
-  int rem = pl.L_eff - dtc::kTileBits;
-  int n_hi = (rem + 7) / 8;
-  int s = dtc::kTileBits;
+  pl.diag_stride = (pl.n_chunks + pl.L_eff) * 64;
+  int hi_max = 9;
+  if (const char* e = std::getenv("DTC_HI_SITES")) hi_max = std::max(1, std::min(9, std::atoi(e)));
+  if (L <= dtc::kTileBits) {
+    // one group; the padding sites L..11 get identity kicks (kernel) so the
+    // whole 12-bit tile runs the standard round plan
+    pl.groups.push_back(Group{0, 0, (1 << dtc::kTileBits) - 1});
+    return pl;
+  }
+  const int rem0 = L - dtc::kTileBits;
+  const int n_hi = (rem0 + hi_max - 1) / hi_max;
+  // lo group keeps the rest so the hi groups are as full as allowed
+  int a_lo = L - std::min(rem0 + 0, n_hi * hi_max);
+  a_lo = std::max(a_lo, L - n_hi * hi_max);
+  a_lo = std::min(a_lo, dtc::kTileBits);
+  if (const char* e = std::getenv("DTC_LO_SITES")) {
+    int v = std::atoi(e);
+    if (v >= L - n_hi * hi_max && v <= dtc::kTileBits) a_lo = v;
+  }
+  pl.groups.push_back(Group{0, 0, (1 << a_lo) - 1});
+  int s = a_lo, rem = L - a_lo;
   for (int i = 0; i < n_hi; ++i) {
-    int a = (rem + (n_hi - i) - 1) / (n_hi - i);  // even split, larger first
-    pl.hi.push_back(Geom{dtc::kTileBits - a, s, a});
+    const int a = (rem + (n_hi - i) - 1) / (n_hi - i);
+    const int c = dtc::kTileBits - a;
+    pl.groups.push_back(Group{c, s, ((1 << a) - 1) << c});
     s += a;
     rem -= a;
   }
@@ -151,9 +180,10 @@ Plan make_plan(int L) {
 // Diagonal factor tables (RZZ even/odd bonds + RZ, fast.py:115-120):
 // D(x) = exp(-i/2 (sum_i h_i z_i + sum_i phi_i z_i z_{i+1})), z_i = 1 - 2 bit_i(x).
 // Per instance: n_chunks chunk tables, D(x) = prod_k C_k[(x >> 5k) & 63] (C_k covers
-// sites 5k..5k+4 and the bond to site 5k+5 = index bit 5), followed by 3 register-
-// nibble tables N_n[v], v = bits [4n-1, 4n+5) of x, holding the terms of sites
-// 4n..4n+3 and of the bonds touching them (the kernel's apply_diag_nibble<n>).
+// sites 5k..5k+4 and the bond to site 5k+5 = index bit 5), followed by one window
+// table W_g0[v] per start bit g0, v = bits [g0-1, g0+5) of x, holding the terms of
+// sites g0..g0+3 and of every bond touching them (the kernel factors
+// D(x) = D(x0) / W(x0) * W(x) over the 16 amplitudes of a thread).
 double diag_angle(int L, const double* hh, const double* pp, int lo_site, int hi_site,
                   int bond_lo, int bond_hi, int bit0, int v) {
   auto z = [&](int i) -> double { return ((v >> (i - bit0)) & 1) ? -1.0 : 1.0; };
@@ -166,29 +196,26 @@ double diag_angle(int L, const double* hh, const double* pp, int lo_site, int hi
 void build_diag_tables(const Plan& pl, int n_inst, const double* h, const double* phi,
                        std::vector<double>& out) {
   const int L = pl.L;
-  const int per_inst = (pl.n_chunks + 3) * 64;
-  out.assign((size_t)n_inst * per_inst * 2, 0.0);
+  out.assign((size_t)n_inst * pl.diag_stride * 2, 0.0);
   for (int in = 0; in < n_inst; ++in) {
     const double* hh = h + (size_t)in * L;
     const double* pp = phi + (size_t)in * (L > 1 ? L - 1 : 0);
-    double* o = out.data() + (size_t)in * per_inst * 2;
+    double* o = out.data() + (size_t)in * pl.diag_stride * 2;
+    auto put = [&](int e, double ang) {
+      o[e * 2] = std::cos(-0.5 * ang);
+      o[e * 2 + 1] = std::sin(-0.5 * ang);
+    };
     for (int k = 0; k < pl.n_chunks; ++k) {
       const int b0 = dtc::kChunkBits * k;
-      for (int v = 0; v < 64; ++v) {
-        const double ang = diag_angle(L, hh, pp, b0, b0 + dtc::kChunkBits, b0,
-                                      b0 + dtc::kChunkBits, b0, v);
-        o[(k * 64 + v) * 2] = std::cos(-0.5 * ang);
-        o[(k * 64 + v) * 2 + 1] = std::sin(-0.5 * ang);
-      }
+      for (int v = 0; v < 64; ++v)
+        put(k * 64 + v, diag_angle(L, hh, pp, b0, b0 + dtc::kChunkBits, b0,
+                                   b0 + dtc::kChunkBits, b0, v));
     }
-    for (int n = 0; n < 3; ++n) {
-      const int b0 = 4 * n - 1;
+    for (int g0 = 0; g0 < pl.L_eff; ++g0) {
       for (int v = 0; v < 64; ++v) {
-        if (n == 0 && (v & 1)) continue;  // bit -1 does not exist
-        const double ang = diag_angle(L, hh, pp, 4 * n, 4 * n + 4, 4 * n - 1, 4 * n + 4, b0, v);
-        const int e = (pl.n_chunks + n) * 64 + v;
-        o[e * 2] = std::cos(-0.5 * ang);
-        o[e * 2 + 1] = std::sin(-0.5 * ang);
+        if (g0 == 0 && (v & 1)) continue;  // bit -1 does not exist
+        put((pl.n_chunks + g0) * 64 + v,
+            diag_angle(L, hh, pp, g0, g0 + 4, g0 - 1, g0 + 4, g0 - 1, v));
       }
     }
   }
@@ -197,12 +224,58 @@ void build_diag_tables(const Plan& pl, int n_inst, const double* h, const double
 struct RunCfg {
   const dtc_problem* prob;
   Plan pl;
+  std::vector<int> row_kind;  // KickKind of every kick-table row
   uint64_t seed;
   int64_t traj_offset;
   int n_traj;
   int noisy;
   uint32_t thr1, thr2, thr3;
 };
+
+// ---- layer chains ---------------------------------------------------------
+using dtc::KickDesc;
+
+KickDesc no_kick() { return KickDesc{0, 0, 0, 0u, 0u}; }
+
+struct Chain {
+  std::vector<KickDesc> X;  // kick layers X_0..X_n
+  bool trailing_d = false;  // a D after X_n too
+  int diag = dtc::kDiagFwd;
+  std::vector<int> kc;      // layers applied per group
+  int nd = 0;               // diagonals applied
+  int n() const { return (int)X.size() - 1; }
+  int n_d() const { return trailing_d ? n() + 1 : n(); }
+  bool done() const {
+    if (nd != n_d()) return false;
+    for (int k : kc)
+      if (k != n() + 1) return false;
+    return true;
+  }
+};
+
+struct PassSpec {
+  int group;
+  KickDesc pre, post;
+  int diag;    // DiagMode
+  int d_index; // diagonals applied after this pass (valid when diag)
+};
+
+// Emit the next pass of a chain (greedy, deterministic).
+PassSpec next_pass(Chain& ch) {
+  const int G = (int)(std::min_element(ch.kc.begin(), ch.kc.end()) - ch.kc.begin());
+  PassSpec ps{G, no_kick(), no_kick(), dtc::kDiagNone, ch.nd};
+  const int n = ch.n();
+  if (ch.kc[G] == ch.nd && ch.kc[G] <= n) ps.pre = ch.X[ch.kc[G]++];
+  bool level = true;
+  for (int k : ch.kc)
+    if (k != ch.nd + 1) level = false;
+  if (level && ch.nd < ch.n_d()) {
+    ps.diag = ch.diag;
+    ps.d_index = ++ch.nd;
+    if (ch.kc[G] == ch.nd && ch.kc[G] <= n) ps.post = ch.X[ch.kc[G]++];
+  }
+  return ps;
+}
 
 dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   dtc::PassArgs A{};
@@ -221,29 +294,10 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.noisy = rc.noisy;
   A.diag = (const double2*)ctx->diag.p;
   A.n_chunks = rc.pl.n_chunks;
+  A.diag_stride = rc.pl.diag_stride;
   A.probe = rc.prob->probe_site;
   A.partial = (double*)ctx->partial.p;
   return A;
-}
-
-int launch_one(dtc_ctx* ctx, dtc::PassArgs A, const Geom& g, int batch, int diag_mode,
-               int meas_mode, int kind) {
-  A.c = g.c;
-  A.s = g.s;
-  A.a = g.a;
-  A.tile_bits_mid = g.s - g.c;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (ctx->prof) {
-    e0 = get_event(ctx);
-    e1 = get_event(ctx);
-    DTC_HIP(hipEventRecord(e0, ctx->stream));
-  }
-  DTC_HIP(dtc::launch_pass(A, batch, diag_mode, meas_mode, ctx->stream));
-  if (ctx->prof) {
-    DTC_HIP(hipEventRecord(e1, ctx->stream));
-    ctx->pending.push_back(Pending{kind, e0, e1, 32.0 * (double)A.state_len * batch});
-  }
-  return DTC_OK;
 }
 
 int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* out,
@@ -264,63 +318,123 @@ int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* 
   return DTC_OK;
 }
 
-// One forward period p (1-based) on `batch` states: K_hi passes, then the fused
-// K_lo + diagonal pass (fast.py:111-121 order: kicks, RZZ, RZ).
-int forward_period(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
-                   const double2* src, double2* dst, int p, uint32_t stream, int meas_mode,
-                   int n_obs, double* meas_out, int64_t meas_stride) {
+// Launch one pass; if meas_mode != none, reduce its observables into meas_out.
+int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
+                     const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
+                     int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride) {
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
-  A.kick_row = p - 1;
-  A.inverse = 0;
-  A.stream = stream;
-  A.rng_period = (uint32_t)p;
-  A.n_obs = n_obs;
-  const double2* s = src;
-  for (const Geom& g : rc.pl.hi) {
-    A.src = s;
-    A.dst = dst;
-    DTC_TRY(launch_one(ctx, A, g, batch, dtc::kDiagNone, dtc::kMeasNone, DTC_KERNEL_HI_PASS));
-    s = dst;
-  }
-  A.src = s;
+  const Group& g = rc.pl.groups[ps.group];
+  A.src = src;
   A.dst = dst;
-  DTC_TRY(launch_one(ctx, A, rc.pl.lo, batch, dtc::kDiagAfter, meas_mode, DTC_KERNEL_LO_PASS));
+  A.c = g.c;
+  A.s = g.s;
+  A.tile_bits_mid = g.s - g.c;
+  A.act = g.act;
+  A.pre = ps.pre;
+  A.post = ps.post;
+  A.diag_conj = ps.diag == dtc::kDiagConj;
+  A.meas = meas_mode;
+  A.meas_at_end = meas_at_end;
+  A.n_obs = n_obs;
+  const bool has_d = ps.diag != dtc::kDiagNone;
+  int shape;
+  if (ps.pre.enabled && has_d && ps.post.enabled) shape = dtc::kShapeKDK;
+  else if (ps.pre.enabled && has_d) shape = dtc::kShapeKD;
+  else if (has_d && ps.post.enabled) shape = dtc::kShapeDK;
+  else if (ps.pre.enabled && !has_d && !ps.post.enabled) shape = dtc::kShapeK;
+  else if (has_d) shape = dtc::kShapeD;
+  else return fail(DTC_EINVAL, "internal: empty pass");
+  int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
+  for (const KickDesc* k : {&ps.pre, &ps.post}) {
+    if (!k->enabled) continue;
+    const int rk = rc.row_kind[k->row];
+    kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
+  }
+  const int kernel = has_d ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->prof) {
+    e0 = get_event(ctx);
+    e1 = get_event(ctx);
+    DTC_HIP(hipEventRecord(e0, ctx->stream));
+  }
+  DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream));
+  if (ctx->prof) {
+    DTC_HIP(hipEventRecord(e1, ctx->stream));
+    ctx->pending.push_back(Pending{kernel, e0, e1, 32.0 * (double)A.state_len * batch});
+  }
   if (meas_mode != dtc::kMeasNone)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
   return DTC_OK;
 }
 
-// One inverse period (fast.py:140-143, UF.inverse()): diagonal^-1 fused into
-// the K_lo pass, then K_hi passes; rng counter = echo step k.
-int inverse_period(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
-                   const double2* src, double2* dst, int p, int step, uint32_t stream,
-                   int meas_mode, int n_obs, double* meas_out, int64_t meas_stride) {
-  dtc::PassArgs A = base_args(ctx, rc, batch_start);
-  A.kick_row = p - 1;
-  A.inverse = 1;
-  A.stream = stream;
-  A.rng_period = (uint32_t)step;
-  A.n_obs = n_obs;
-  const bool lo_last = rc.pl.hi.empty();
-  A.src = src;
-  A.dst = dst;
-  DTC_TRY(launch_one(ctx, A, rc.pl.lo, batch, dtc::kDiagBeforeConj,
-                     lo_last ? meas_mode : dtc::kMeasNone, DTC_KERNEL_LO_PASS));
-  for (size_t i = 0; i < rc.pl.hi.size(); ++i) {
-    A.src = dst;
-    A.dst = dst;
-    const bool last = (i + 1 == rc.pl.hi.size());
-    DTC_TRY(launch_one(ctx, A, rc.pl.hi[i], batch, dtc::kDiagNone,
-                       last ? meas_mode : dtc::kMeasNone, DTC_KERNEL_HI_PASS));
+// Matrix family of each kick-table row: RX if every sub-gate is
+// [[real, imag], [imag, real]], RY if every sub-gate is real, else general.
+// Both families are closed under products, Paulis and daggers.
+std::vector<int> classify_rows(const dtc_problem* pr) {
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  std::vector<int> out(n_rows);
+  const size_t per_row = (size_t)pr->L * pr->n_sub;
+  for (int r = 0; r < n_rows; ++r) {
+    bool rx = true, ry = true;
+    for (size_t e = 0; e < per_row; ++e) {
+      const double* m = pr->kick + ((size_t)r * per_row + e) * 8;
+      // m = {m00.re, m00.im, m01.re, m01.im, m10.re, m10.im, m11.re, m11.im}
+      if (!(m[1] == 0.0 && m[2] == 0.0 && m[4] == 0.0 && m[7] == 0.0)) rx = false;
+      if (!(m[1] == 0.0 && m[3] == 0.0 && m[5] == 0.0 && m[7] == 0.0)) ry = false;
+    }
+    out[r] = rx ? dtc::kKindRX : (ry ? dtc::kKindRY : dtc::kKindGen);
   }
-  if (meas_mode != dtc::kMeasNone)
-    DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
+  return out;
+}
+
+// Forward chain over periods first .. first + n - 1 (rows period-1, RNG counter
+// = period, stream `stream`), a diagonal after every layer (fast.py:111-121).
+Chain forward_chain(const Plan& pl, int first, int n, uint32_t stream) {
+  Chain ch;
+  for (int k = 0; k < n; ++k)
+    ch.X.push_back(KickDesc{1, first + k - 1, dtc::kKickForward, stream, (uint32_t)(first + k)});
+  ch.trailing_d = true;
+  ch.diag = dtc::kDiagFwd;
+  ch.kc.assign(pl.groups.size(), 0);
+  return ch;
+}
+
+// Echo chain (fast.py:140-143, UF.inverse() per period, periods in reverse):
+// D^* K'_p D^* K'_{p-1} ... D^* K'_1, RNG stream `stream`, counter = step k.
+// `ahead[g]` marks groups whose state already carries the forward layer
+// K_{p+1} (row p): X_0 undoes it exactly before the first D^*.
+Chain echo_chain(const Plan& pl, int p, uint32_t stream, const std::vector<int>& ahead) {
+  Chain ch;
+  ch.X.push_back(KickDesc{1, p, dtc::kKickUndo, dtc::kStreamForward, (uint32_t)(p + 1)});
+  for (int k = 1; k <= p; ++k)
+    ch.X.push_back(KickDesc{1, p - k, dtc::kKickInverse, stream, (uint32_t)k});
+  ch.trailing_d = false;
+  ch.diag = dtc::kDiagConj;
+  ch.kc.resize(pl.groups.size());
+  for (size_t g = 0; g < pl.groups.size(); ++g) ch.kc[g] = ahead[g] ? 0 : 1;
+  return ch;
+}
+
+// Run a whole chain; the first pass reads src, every pass writes dst; the
+// observables of the final state are reduced into meas_out (if meas_mode).
+int run_chain(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch, Chain& ch,
+              const double2* src, double2* dst, int meas_mode, int n_obs, double* meas_out,
+              int64_t meas_stride) {
+  const double2* s = src;
+  while (!ch.done()) {
+    PassSpec ps = next_pass(ch);
+    const bool last = ch.done();
+    DTC_TRY(launch_pass_spec(ctx, rc, batch_start, batch, ps, s, dst,
+                             last ? meas_mode : dtc::kMeasNone, 1, n_obs, meas_out,
+                             meas_stride));
+    s = dst;
+  }
   return DTC_OK;
 }
 
 int check_problem(const dtc_problem* pr, const dtc_noise* nz) {
   if (!pr || !nz) return fail(DTC_EINVAL, "null problem/noise");
-  if (pr->L < 1 || pr->L > 36) return fail(DTC_EINVAL, "L must be in [1, 36]");
+  if (pr->L < 1 || pr->L > 32) return fail(DTC_EINVAL, "L must be in [1, 32] per device");
   if (pr->T < 1) return fail(DTC_EINVAL, "T must be >= 1");
   if (pr->n_inst < 1) return fail(DTC_EINVAL, "n_inst must be >= 1");
   if (pr->probe_site < 0 || pr->probe_site >= pr->L)
@@ -486,6 +600,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   rc.traj_offset = traj_offset;
   rc.n_traj = n_traj;
   rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
   thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
   const Plan& pl = rc.pl;
   const int T = pr->T, L = pr->L;
@@ -543,22 +658,26 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
       DTC_HIP(hipMemsetAsync(ctx->vals_e.p, 0, (size_t)nb * T * 2 * sizeof(double),
                              ctx->stream));
 
-    for (int p = 0; p <= P; ++p) {
-      const int t = p - pr->t_offset;
-      if (p > 0) {
-        const bool meas = want_f && t >= 0 && t >= pr->t_first;
-        DTC_TRY(forward_period(ctx, rc, bs, nb, F, F, p, dtc::kStreamForward,
-                               meas ? meas_f : dtc::kMeasNone, n_obs_f,
-                               meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
-                               (int64_t)T * n_obs_f));
-      }
-      if (t < 0 || t < pr->t_first || !want_e || p == 0) continue;
-      double* vout = (double*)ctx->vals_e.p + (size_t)t * 2;
-      for (int k = 1; k <= p; ++k) {
-        const bool last = (k == p);
-        DTC_TRY(inverse_period(ctx, rc, bs, nb, k == 1 ? F : E, E, p - k + 1, k,
-                               (uint32_t)(1 + t), last ? dtc::kMeasProbe : dtc::kMeasNone, 2,
-                               last ? vout : nullptr, (int64_t)T * 2));
+    // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
+    // and branch the echo at t off F.
+    if (P > 0) {
+      Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
+      while (!fw.done()) {
+        PassSpec ps = next_pass(fw);
+        const int p = ps.d_index;
+        const int t = p - pr->t_offset;
+        const bool closes = ps.diag != dtc::kDiagNone;
+        const bool meas = closes && want_f && t >= 0 && t >= pr->t_first;
+        DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, ps, F, F, meas ? meas_f : dtc::kMeasNone, 0,
+                                 n_obs_f,
+                                 meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
+                                 (int64_t)T * n_obs_f));
+        if (!closes || !want_e || t < 0 || t < pr->t_first) continue;
+        std::vector<int> ahead(pl.groups.size());
+        for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > p;
+        Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
+        DTC_TRY(run_chain(ctx, rc, bs, nb, ec, F, E, dtc::kMeasProbe, 2,
+                          (double*)ctx->vals_e.p + (size_t)t * 2, (int64_t)T * 2));
       }
     }
     DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
@@ -616,6 +735,7 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
   rc.traj_offset = traj;
   rc.n_traj = 1;
   rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
   thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
   const Plan& pl = rc.pl;
   const int L = pr->L;
@@ -627,17 +747,22 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
   DTC_HIP(hipMemsetAsync(F, 0, (size_t)pl.len * 16, ctx->stream));
   DTC_HIP(hipMemcpyAsync(F, state, ((size_t)1 << L) * 16, hipMemcpyHostToDevice, ctx->stream));
   const int64_t batch_start = inst;  // n_traj = 1: g = inst -> (inst, traj)
-  for (int k = 1; k <= n_periods; ++k) {
-    const bool last = (k == n_periods) && zsite_out;
-    const int meas = last ? dtc::kMeasSites : dtc::kMeasNone;
+  if (n_periods > 0) {
+    Chain ch;
     if (inverse) {
-      DTC_TRY(inverse_period(ctx, rc, batch_start, 1, F, F, first_period - k + 1, k, stream, meas,
-                             1 + L, (double*)ctx->vals_f.p, 1 + L));
+      ch = echo_chain(pl, first_period, stream, std::vector<int>(pl.groups.size(), 0));
+      // echo_chain counts periods p..1; re-base so the first inverse period is
+      // first_period and there are n_periods of them
+      ch.X.resize(1);
+      for (int k = 1; k <= n_periods; ++k)
+        ch.X.push_back(dtc::KickDesc{1, first_period - k, dtc::kKickInverse, stream,
+                                     (uint32_t)k});
     } else {
-      const int p = first_period + k - 1;
-      DTC_TRY(forward_period(ctx, rc, batch_start, 1, F, F, p, stream, meas, 1 + L,
-                             (double*)ctx->vals_f.p, 1 + L));
+      ch = forward_chain(pl, first_period, n_periods, stream);
     }
+    DTC_TRY(run_chain(ctx, rc, batch_start, 1, ch, F, F,
+                      zsite_out ? dtc::kMeasSites : dtc::kMeasNone, 1 + L,
+                      (double*)ctx->vals_f.p, 1 + L));
   }
   DTC_HIP(hipMemcpyAsync(state, F, ((size_t)1 << L) * 16, hipMemcpyDeviceToHost, ctx->stream));
   if (zsite_out && n_periods > 0)

@@ -16,20 +16,46 @@ static constexpr int kChunkBits = 5;      // diagonal factor tables: 5 sites + n
 static constexpr int kMaxChunks = 8;      // L_eff <= 40
 static constexpr int kMaxObs = 1 + 40;    // norm + per-site <Z_i>
 
-enum DiagMode { kDiagNone = 0, kDiagAfter = 1, kDiagBeforeConj = 2 };
+enum DiagMode { kDiagNone = 0, kDiagFwd = 1, kDiagConj = 2 };
 enum MeasMode { kMeasNone = 0, kMeasProbe = 1, kMeasSites = 2 };
+// Which parts a pass runs: pre-kick (K), diagonal (D), post-kick (K).
+enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4 };
+// Matrix family of every kick in a pass (chosen by the host from the kick
+// table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
+// i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
+enum KickKind { kKindRX = 0, kKindRY = 1, kKindGen = 2 };
 
-// One pass over a batch of states: a tile covers the index bits
-// [0, c) ∪ [s, s + a) with c + a = kTileBits; the kick gates of sites
-// s .. s+a-1 are applied (sites >= L_real are padding: identity).
+// One layer of single-site kicks on the sites of a pass.
+enum KickMode {
+  kKickForward = 0,  // M = P_n G_n ... P_1 G_1            (forward period, noisy)
+  kKickInverse = 1,  // M = P_n G_1^+ ... P_1 G_n^+        (UF.inverse(), noisy)
+  kKickUndo = 2,     // M = (forward M)^+                  (exact undo, same draws)
+};
+
+struct KickDesc {
+  int enabled;
+  int row;              // kick table row (period - 1)
+  int mode;             // KickMode
+  uint32_t stream;      // RNG stream (0 forward, 1 + t echo branch at t)
+  uint32_t rng_period;  // RNG period counter
+};
+
+// One streaming pass over a batch of states.  A tile covers index bits
+// [0, c) ∪ [s, s + 12 - c); tile bit k < c is global bit k, tile bit k >= c is
+// global bit s + k - c.  The pass applies, in order:
+//   pre-kick on the active tile bits -> diagonal D or D^* -> (measure) ->
+//   post-kick on the active tile bits
+// (any part optional), so one pass can finish period p on its sites, close
+// the period with the diagonal and start period p+1 ("K-D-K" pass).
 struct PassArgs {
   const double2* src;      // batch base, state b at src + b * state_len
   double2* dst;            // may alias src (in-place)
   int64_t state_len;       // 2^L_eff
   int L_eff;               // padded number of index bits (>= kTileBits)
   int L_real;              // physical sites
-  int c, s, a;             // tile geometry
+  int c, s;                // tile geometry
   int tile_bits_mid;       // s - c  (tile-id bits deposited at [c, s))
+  int act;                 // active tile-bit mask (sites kicked by this pass)
   // batch -> (instance, trajectory)
   int64_t batch_start;
   int n_traj;
@@ -37,25 +63,27 @@ struct PassArgs {
   // kicks
   const double2* kick;     // [n_periods][L_real][n_sub][4]
   int n_sub;
-  int kick_row;            // row of the kick table for this period
-  int inverse;             // apply (G_q)^dagger in reverse sub order
+  KickDesc pre, post;
   // noise
   uint32_t thr1, thr2, thr3;
   uint64_t seed;
-  uint32_t stream;
-  uint32_t rng_period;
   int noisy;
-  // diagonal factor tables [n_inst][n_chunks][64]
+  // diagonal factor tables, per instance: n_chunks chunk tables then one
+  // 64-entry window table per start bit g0 = 0 .. L_eff-1
   const double2* diag;
   int n_chunks;
+  int diag_stride;         // double2 entries per instance
   // measurement
+  int diag_conj;           // apply D^* instead of D
+  int meas;                // MeasMode
   int probe;
+  int meas_at_end;         // measure after the post-kick instead of after the diagonal
   int n_obs;               // kMeasProbe: 2 (norm, Z_probe); kMeasSites: 1 + L_real
   double* partial;         // [B][n_tiles][n_obs]
 };
 
-hipError_t launch_pass(const PassArgs& a, int batch, int diag_mode, int meas_mode,
-                       hipStream_t stream);
+// act must cover nibble sets {2}, {1,2} or {0,1,2}; L_eff in [12, 32].
+hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);
 
 // out[b * out_stride + o] = sum over tiles of partial[b][tile][o] (fixed order)
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,

@@ -5,18 +5,27 @@
 //   RZ(h_i) on every site,
 // with a Pauli draw after every kick gate (depolarizing noise on u3,
 // fast.py:84-86).  The inverse period (fast.py:140-143) is RZ(-h), RZZ(-phi),
-// RX(-pi g) with noise after each kick.  Single-site kicks on different sites
-// commute, and RZZ/RZ are one diagonal D(x), so a period is
-//     D . K_lo . K_hi      (forward)      K'_hi . K'_lo . D^*   (inverse)
-// where K_lo acts on sites 0..11 and K_hi on the rest.  Each factor group is
-// one streaming pass over the state: a workgroup loads a 4096-amplitude tile
-// (16 amplitudes per lane, coalesced 16-B loads), applies the 2x2 kick of
-// every site whose bit lies in the tile as register butterflies, re-layouts
-// the tile through 64 KiB of bank-conflict-free (XOR-swizzled) LDS between
-// 4-site rounds, applies the diagonal from per-instance LDS factor tables,
-// optionally reduces |a|^2 Z_i for the autocorrelator, and stores the tile
-// back.  Memory-bound by design: 32 B of HBM traffic per amplitude per pass,
-// no MFMA (complex128 butterflies are not GEMM-shaped).
+// RX(-pi g) with noise after each kick.
+//
+// Kicks on different sites commute and RZZ/RZ form one diagonal D(x), so a
+// sweep is the layer sequence K_1 D K_2 D K_3 ...  The sites are split in two
+// groups A (low index bits) and B (high bits) whose kicks fit a 4096-amplitude
+// tile each.  A pass over group G applies K_{p,G} . D . K_{p+1,G}: it finishes
+// period p on G (the other group already has K_p), closes the period with the
+// diagonal, and starts period p+1 on G.  Passes alternate A, B, A, ... so every
+// pass advances one full period: 32 B of HBM traffic per amplitude per period.
+//
+// Inside a pass a workgroup loads its tile (16 amplitudes per lane, coalesced
+// 16-B loads), applies each site's 2x2 kick as register butterflies in 4-site
+// rounds, re-layouts the tile through 64 KiB of XOR-swizzled (bank-conflict
+// free) LDS between rounds, applies the diagonal from per-instance LDS factor
+// tables, optionally reduces |a|^2 Z_i for the autocorrelator, and stores the
+// tile back.  Memory-bound by design; no MFMA (complex128 butterflies are not
+// GEMM-shaped).  Kicks of the RX family (every Pauli x RX(theta) has one real
+// and one imaginary entry per row) run as 4-flop-per-amplitude butterflies;
+// other kicks (RY products, circular polarization) use the general form.
+#include <type_traits>
+
 #include "dtc_kernels.h"
 #include "dtc_rng.h"
 
@@ -26,14 +35,38 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-// (u, v) <- (m00 u + m01 v, m10 u + m11 v)
-__device__ __forceinline__ void butterfly(double2& u, double2& v, const double2* m) {
+// General: (u, v) <- (m00 u + m01 v, m10 u + m11 v)
+__device__ __forceinline__ void bfly_general(double2& u, double2& v, const double2* m) {
   const double2 m00 = m[0], m01 = m[1], m10 = m[2], m11 = m[3];
   double2 nu, nv;
   nu.x = m00.x * u.x - m00.y * u.y + m01.x * v.x - m01.y * v.y;
   nu.y = m00.x * u.y + m00.y * u.x + m01.x * v.y + m01.y * v.x;
   nv.x = m10.x * u.x - m10.y * u.y + m11.x * v.x - m11.y * v.y;
   nv.y = m10.x * u.y + m10.y * u.x + m11.x * v.y + m11.y * v.x;
+  u = nu;
+  v = nv;
+}
+
+// RX family: [[a, i b], [i c, d]] (a, b, c, d real) — 4 flops per amplitude
+__device__ __forceinline__ void bfly_rx(double2& u, double2& v, double a, double b, double c,
+                                        double d) {
+  double2 nu, nv;
+  nu.x = a * u.x - b * v.y;
+  nu.y = a * u.y + b * v.x;
+  nv.x = d * v.x - c * u.y;
+  nv.y = d * v.y + c * u.x;
+  u = nu;
+  v = nv;
+}
+
+// RY family: [[a, b], [c, d]] real
+__device__ __forceinline__ void bfly_ry(double2& u, double2& v, double a, double b, double c,
+                                        double d) {
+  double2 nu, nv;
+  nu.x = a * u.x + b * v.x;
+  nu.y = a * u.y + b * v.y;
+  nv.x = c * u.x + d * v.x;
+  nv.y = c * u.y + d * v.y;
   u = nu;
   v = nv;
 }
@@ -68,92 +101,146 @@ __device__ __forceinline__ void mat_mul(double2* c, const double2* a, const doub
   for (int k = 0; k < 4; ++k) c[k] = r[k];
 }
 
-// Noisy kick of one site for one period: M = P_n G_n ... P_1 G_1.
-__device__ void build_site_kick(const PassArgs& A, int site, uint64_t traj, double2* m) {
+__device__ __forceinline__ void dagger(double2* m) {
+  double2 m01 = m[1];
+  m[0].y = -m[0].y;
+  m[3].y = -m[3].y;
+  m[1] = make_double2(m[2].x, -m[2].y);
+  m[2] = make_double2(m01.x, -m01.y);
+}
+
+// Noisy kick of one site for one layer (see KickMode).
+__device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, uint64_t traj,
+                                double2* m) {
   m[0] = make_double2(1.0, 0.0);
   m[1] = make_double2(0.0, 0.0);
   m[2] = make_double2(0.0, 0.0);
   m[3] = make_double2(1.0, 0.0);
+  const bool inv = (K.mode == kKickInverse);
   for (int q = 0; q < A.n_sub; ++q) {
-    const int qq = A.inverse ? (A.n_sub - 1 - q) : q;
-    const double2* gp = A.kick + (((int64_t)A.kick_row * A.L_real + site) * A.n_sub + qq) * 4;
-    double2 gm[4];
-    if (A.inverse) {  // G^dagger
-      gm[0] = make_double2(gp[0].x, -gp[0].y);
-      gm[1] = make_double2(gp[2].x, -gp[2].y);
-      gm[2] = make_double2(gp[1].x, -gp[1].y);
-      gm[3] = make_double2(gp[3].x, -gp[3].y);
-    } else {
-      gm[0] = gp[0]; gm[1] = gp[1]; gm[2] = gp[2]; gm[3] = gp[3];
-    }
+    const int qq = inv ? (A.n_sub - 1 - q) : q;
+    const double2* gp = A.kick + (((int64_t)K.row * A.L_real + site) * A.n_sub + qq) * 4;
+    double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
+    if (inv) dagger(gm);
     mat_mul(m, gm, m);
     if (A.noisy) {
-      int p = sample_pauli(A.seed, traj, A.stream, A.rng_period, (uint32_t)site, (uint32_t)q,
+      int p = sample_pauli(A.seed, traj, K.stream, K.rng_period, (uint32_t)site, (uint32_t)q,
                            A.thr1, A.thr2, A.thr3);
       pauli_left(m, p);
     }
   }
+  if (K.mode == kKickUndo) dagger(m);
 }
 
-// Tile layouts: register r of lane-thread t holds tile index Y(t, r).
+// Per-site kick of a pass, canonicalised for the pass's matrix family:
+//   RX: M = i^k [[a, i b], [i c, d]]   (Pauli x RX(theta): k = 1 for X errors)
+//   RY: M = i^k [[a, b], [c, d]]       (Pauli x RY(theta): k = 1 for Y errors)
+//   general: M = m (k = 0)
+// The global phases i^k of all sites are multiplied into the diagonal.
+struct SiteMat {
+  double2 m[4];  // general form; RX/RY use m[0].x..m[1].y as a, b, c, d
+  int k;         // power of i
+};
+
+__device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat& sm) {
+  sm.k = 0;
+  if (kind == kKindRX) {
+    const bool a_form = (m[0].y == 0.0 && m[1].x == 0.0 && m[2].x == 0.0 && m[3].y == 0.0);
+    // B form [[i a, b], [c, i d]] = i [[a, -i b], [-i c, d]]
+    const double a = a_form ? m[0].x : m[0].y;
+    const double b = a_form ? m[1].y : -m[1].x;
+    const double c = a_form ? m[2].y : -m[2].x;
+    const double d = a_form ? m[3].x : m[3].y;
+    sm.m[0] = make_double2(a, b);
+    sm.m[1] = make_double2(c, d);
+    sm.k = a_form ? 0 : 1;
+  } else if (kind == kKindRY) {
+    const bool real = (m[0].y == 0.0 && m[1].y == 0.0 && m[2].y == 0.0 && m[3].y == 0.0);
+    // imaginary form i [[a, b], [c, d]]
+    sm.m[0] = make_double2(real ? m[0].x : m[0].y, real ? m[1].x : m[1].y);
+    sm.m[1] = make_double2(real ? m[2].x : m[2].y, real ? m[3].x : m[3].y);
+    sm.k = real ? 0 : 1;
+  } else {
+    for (int e = 0; e < 4; ++e) sm.m[e] = m[e];
+  }
+}
+
+// Tile layouts: register r of lane-thread t holds tile index Y(t, r) =
+// ybase<LAY>(t) | (r << 4 LAY).
 // Layout 2: registers = tile bits 8..11, threads = bits 0..7 (coalesced).
 // Layout 1: registers = tile bits 4..7.  Layout 0: registers = bits 0..3.
-__device__ __forceinline__ int tile_y(int layout, int t, int r) {
-  if (layout == 2) return t | (r << 8);
-  if (layout == 1) return (t & 15) | (r << 4) | ((t >> 4) << 8);
-  return r | (t << 4);
+template <int LAY>
+__device__ __forceinline__ int ybase(int t) {
+  if (LAY == 2) return t;
+  if (LAY == 1) return (t & 15) | ((t >> 4) << 8);
+  return t << 4;
+}
+template <int LAY>
+__device__ __forceinline__ int tile_y(int t, int r) {
+  return ybase<LAY>(t) | (r << (4 * LAY));
 }
 
 // XOR swizzle over 16-B slots: conflict-free ds_write_b128 / ds_read_b128 for
 // every layout transition used here (MI355X_MICROARCH.md §LDS lane groups).
 __device__ __forceinline__ int lds_slot(int y) { return y ^ ((y >> 4) & 15); }
 
-template <int N>
-__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const double2 (*s_mat)[4],
-                                             int act) {
+// Wave-uniform copy of an LDS value (the matrices are identical across the
+// workgroup): SGPR coefficients, no per-lane copies.
+__device__ __forceinline__ double uni(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int N, int KIND>
+__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const SiteMat* s_mat, int act) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int k = 4 * N + q;
     if (act & (1 << k)) {
-      double2 m[4];
-      m[0] = s_mat[k][0]; m[1] = s_mat[k][1]; m[2] = s_mat[k][2]; m[3] = s_mat[k][3];
+      // keep the scheduler from hoisting every layer's coefficient loads to
+      // the top of the pass (register pressure -> spills)
+      __builtin_amdgcn_sched_barrier(0);
+      if (KIND == kKindGen) {
+        double2 m[4];
 #pragma unroll
-      for (int r = 0; r < kRegs; ++r) {
-        if (!(r & (1 << q))) butterfly(v[r], v[r | (1 << q)], m);
+        for (int e = 0; e < 4; ++e)
+          m[e] = make_double2(uni(s_mat[k].m[e].x), uni(s_mat[k].m[e].y));
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r)
+          if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
+      } else {
+        const double a = uni(s_mat[k].m[0].x), b = uni(s_mat[k].m[0].y);
+        const double c = uni(s_mat[k].m[1].x), d = uni(s_mat[k].m[1].y);
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+          if (r & (1 << q)) continue;
+          if (KIND == kKindRX) bfly_rx(v[r], v[r | (1 << q)], a, b, c, d);
+          else bfly_ry(v[r], v[r | (1 << q)], a, b, c, d);
+        }
       }
     }
   }
 }
 
-__device__ __forceinline__ double2 diag_phase(const double2* s_diag, int n_chunks, int64_t x) {
-  double2 ph = s_diag[x & 63];
+template <int FROM, int TO>
+__device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, int t) {
+  if (FROM == TO) return;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y<FROM>(t, r))] = v[r];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y<TO>(t, r))];
+}
+
+__device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chunks, int64_t x) {
+  double2 ph = s_chunk[x & 63];
   for (int k = 1; k < n_chunks; ++k) {
-    ph = cmul(ph, s_diag[k * 64 + ((x >> (kChunkBits * k)) & 63)]);
+    ph = cmul(ph, s_chunk[k * 64 + ((x >> (kChunkBits * k)) & 63)]);
   }
   return ph;
-}
-
-// Index of the register-nibble table N: bits [4N-1, 4N+5) of x (bit -1 = 0).
-__device__ __forceinline__ int nib_index(int64_t x, int N) {
-  return (int)(((x << 1) >> (4 * N)) & 63);
-}
-
-// Diagonal on the 16 amplitudes of a thread whose registers span global bits
-// [4N, 4N+4) (low pass: tile bits == global bits).  D(x) = P_C * T_N[x], with
-// the thread constant P_C = D(x0) / T_N[x0] computed once: one LDS lookup and
-// two complex products per amplitude instead of n_chunks lookups.
-template <int N>
-__device__ __forceinline__ void apply_diag_nibble(double2 (&v)[kRegs], const double2* s_diag,
-                                                  int n_chunks, int64_t x0) {
-  const double2* tn = s_diag + (n_chunks + N) * 64;
-  const double2 d0 = diag_phase(s_diag, n_chunks, x0);
-  const double2 r0 = tn[nib_index(x0, N)];
-  const double2 pc = cmul(d0, make_double2(r0.x, -r0.y));
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) {
-    const int64_t x = x0 | ((int64_t)r << (4 * N));
-    v[r] = cmul(v[r], cmul(pc, tn[nib_index(x, N)]));
-  }
 }
 
 __device__ __forceinline__ double wave_sum(double x) {
@@ -162,12 +249,44 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-template <int DIAG, int MEAS>
+// Per-layout global index of register r: x(r) = x0(t) | off(r), off uniform.
+struct TileMap {
+  int64_t tbase;
+  int c, s, cmask;
+  __device__ __forceinline__ int64_t rel(int y) const {
+    return (int64_t)(y & cmask) | ((int64_t)(y >> c) << s);
+  }
+  __device__ __forceinline__ int64_t at(int y) const { return tbase | rel(y); }
+};
+
+// Compile-time round plan.  NIBS = register nibbles holding active sites
+// (bit n = nibble n).  Pre-kick rounds 2 -> 0 -> 1 (from the coalesced load
+// layout), diagonal + measurement where the pre-kick ends, post-kick rounds
+// 1 -> 0 -> 2, store from layout 2.
+template <int NIBS, int SHAPE>
+struct RoundPlan {
+  static constexpr bool n0 = NIBS & 1, n1 = NIBS & 2, n2 = NIBS & 4;
+  static constexpr bool pre = SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK;
+  static constexpr bool diag =
+      SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeD;
+  static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK;
+  static constexpr int d_lay = pre ? (n1 ? 1 : (n0 ? 0 : 2)) : 2;
+  // layouts reached by the post rounds
+  static constexpr int p1 = n1 ? 1 : d_lay;
+  static constexpr int p0 = n0 ? 0 : p1;
+  static constexpr int p2 = n2 ? 2 : p0;
+};
+
+template <int SHAPE, int NIBS, int KIND>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
+  using RP = RoundPlan<NIBS, SHAPE>;
   __shared__ double2 s_tile[kTile];
-  __shared__ double2 s_diag[DIAG != kDiagNone ? (kMaxChunks + 3) * 64 : 1];
-  __shared__ double2 s_mat[kTileBits][4];
-  __shared__ double s_red[kThreads / 64][MEAS == kMeasSites ? kMaxObs : 2];
+  __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
+  __shared__ double2 s_win[RP::diag ? 64 : 1];
+  __shared__ SiteMat s_pre[RP::pre ? kTileBits : 1];
+  __shared__ SiteMat s_post[RP::post ? kTileBits : 1];
+  __shared__ int s_k[2 * kTileBits];
+  __shared__ double s_red[kThreads / 64][kMaxObs];
 
   const int t = threadIdx.x;
   const int tile = blockIdx.x;
@@ -175,95 +294,99 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const int64_t g = A.batch_start + b;
   const int inst = (int)(g / A.n_traj);
   const uint64_t traj = (uint64_t)(A.traj_offset + (g % A.n_traj));
-
-  // sites handled by this pass: tile bits [c, 12) -> sites s + (k - c)
-  int act = 0;
-  for (int k = A.c; k < kTileBits; ++k)
-    if (A.s + (k - A.c) < A.L_real) act |= 1 << k;
-
-  if (t < kTileBits) {
-    double2 m[4];
-    if (act & (1 << t)) {
-      build_site_kick(A, A.s + (t - A.c), traj, m);
-    } else {
-      m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
-      m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
-    }
-    s_mat[t][0] = m[0]; s_mat[t][1] = m[1]; s_mat[t][2] = m[2]; s_mat[t][3] = m[3];
-  }
-  if (DIAG != kDiagNone) {
-    const int n_tab = (A.n_chunks + 3) * 64;
-    const double2* dt = A.diag + (int64_t)inst * n_tab;
-    for (int i = t; i < n_tab; i += kThreads) {
-      double2 e = dt[i];
-      if (DIAG == kDiagBeforeConj) e.y = -e.y;
-      s_diag[i] = e;
-    }
-  }
-
-  // tile base: tile-id bits deposited at [c, s) and [s + a, L_eff)
-  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
-  const int64_t tbase = (((int64_t)tile & mid_mask) << A.c) |
-                        (((int64_t)tile >> A.tile_bits_mid) << (A.s + A.a));
-  const int cmask = (1 << A.c) - 1;
+  const int act = A.act;
   const int c = A.c, s = A.s;
-  auto gidx = [&](int y) -> int64_t {
-    return tbase | (int64_t)(y & cmask) | ((int64_t)(y >> c) << s);
-  };
 
-  const double2* src = A.src + (int64_t)b * A.state_len;
+  // tile base: tile-id bits deposited at [c, s) and [s + 12 - c, L_eff)
+  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
+  TileMap M;
+  M.tbase = (((int64_t)tile & mid_mask) << c) |
+            (((int64_t)tile >> A.tile_bits_mid) << (s + kTileBits - c));
+  M.c = c;
+  M.s = s;
+  M.cmask = (1 << c) - 1;
+
+  // Issue the tile loads first; the matrix / table setup below overlaps them.
+  // Address = uniform 64-bit base (tile base + register offset, SGPRs) + one
+  // per-lane 32-bit byte offset shared by all 16 loads (L_eff <= 32).
+  const char* src = (const char*)(A.src + (int64_t)b * A.state_len);
+  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
   double2 v[kRegs];
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r] = src[gidx(tile_y(2, t, r))];
+  for (int r = 0; r < kRegs; ++r)
+    v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
 
-  __syncthreads();  // s_mat, s_diag ready
-
-  if (DIAG == kDiagBeforeConj) apply_diag_nibble<2>(v, s_diag, A.n_chunks, gidx(tile_y(2, t, 0)));
-
-  apply_nibble<2>(v, s_mat, act);
-  int layout = 2;
-  if (act & 0x0F0) {
-    if (act & 0x00F) {
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(0, t, r))];
-      apply_nibble<0>(v, s_mat, act);
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(0, t, r))] = v[r];
-    } else {
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
+  // kick matrices: threads 0..11 pre-kick, 64..75 post-kick (different waves);
+  // sites beyond L (padding of small systems) get the identity
+  if (t < 2 * kTileBits) s_k[t] = 0;
+  {
+    const bool is_pre = RP::pre && t < kTileBits;
+    const bool is_post = RP::post && t >= 64 && t < 64 + kTileBits;
+    const int k = is_pre ? t : t - 64;
+    if ((is_pre || is_post) && (act & (1 << k))) {
+      const KickDesc K = is_pre ? A.pre : A.post;
+      const int site = k < c ? k : s + k - c;
+      double2 m[4];
+      if (site < A.L_real) {
+        build_site_kick(A, K, site, traj, m);
+      } else {
+        m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
+        m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
+      }
+      SiteMat sm;
+      canonicalise(KIND, m, sm);
+      if (is_pre) s_pre[k] = sm;
+      else s_post[k] = sm;
+      atomicAdd(&s_k[0], sm.k);
     }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(1, t, r))];
-    apply_nibble<1>(v, s_mat, act);
-    layout = 1;
-  } else if (act & 0x00F) {
-    // only low sites active (tiny L padded to 12 bits)
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y(2, t, r))] = v[r];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y(0, t, r))];
-    apply_nibble<0>(v, s_mat, act);
-    layout = 0;
   }
+  // diagonal tables: chunk tables + the window table of the layout the
+  // diagonal is applied in (registers = 4 contiguous global bits [g0, g0+4))
+  int g0 = -1;
+  if (RP::diag) {
+    const int tb = 4 * RP::d_lay;
+    if (tb >= c) g0 = s + tb - c;
+    else if (tb + 4 <= c) g0 = tb;
+    const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
+    const double cs = A.diag_conj ? -1.0 : 1.0;
+    for (int i = t; i < A.n_chunks * 64; i += kThreads) {
+      const double2 e = dt[i];
+      s_chunk[i] = make_double2(e.x, cs * e.y);
+    }
+    if (g0 >= 0 && t < 64) {
+      const double2 e = dt[(A.n_chunks + g0) * 64 + t];
+      s_win[t] = make_double2(e.x, cs * e.y);
+    }
+  }
+  __syncthreads();  // matrices, phases and tables ready
+  // global phase i^k of the canonicalised kicks of this pass
+  const int kph = __builtin_amdgcn_readfirstlane(s_k[0]) & 3;
+  const double2 gph = make_double2(kph == 0 ? 1.0 : (kph == 2 ? -1.0 : 0.0),
+                                   kph == 1 ? 1.0 : (kph == 3 ? -1.0 : 0.0));
 
-  if (DIAG == kDiagAfter) {
-    if (layout == 1) {
-      apply_diag_nibble<1>(v, s_diag, A.n_chunks, gidx(tile_y(1, t, 0)));
+  auto diag_in = [&](auto lay_tag) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int64_t x0 = M.at(ybase<LAY>(t));
+    if (g0 >= 0) {
+      // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
+      // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
+      // complex products per amplitude
+      const int w0i = (int)(((x0 << 1) >> g0) & 63);
+      const double2 w0 = s_win[w0i];
+      const double2 pc =
+          cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
     } else {
 #pragma unroll
       for (int r = 0; r < kRegs; ++r)
-        v[r] = cmul(v[r], diag_phase(s_diag, A.n_chunks, gidx(tile_y(layout, t, r))));
+        v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
+                                               x0 | M.rel(r << (4 * LAY)))));
     }
-  }
-
-  if (MEAS != kMeasNone) {
+  };
+  auto measure_in = [&](auto lay_tag) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int64_t x0 = M.at(ybase<LAY>(t));
     const int wave = t >> 6, lane = t & 63;
     double pr[kRegs];
     double ptot = 0.0;
@@ -274,26 +397,17 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
     double tot = wave_sum(ptot);
     if (lane == 0) s_red[wave][0] = tot;
-    if (MEAS == kMeasProbe) {
+    const int n_z = A.meas == kMeasProbe ? 1 : A.L_real;
+    for (int i = 0; i < n_z; ++i) {
+      const int site = A.meas == kMeasProbe ? A.probe : i;
       double z = 0.0;
 #pragma unroll
       for (int r = 0; r < kRegs; ++r) {
-        const int64_t x = gidx(tile_y(layout, t, r));
-        z += ((x >> A.probe) & 1) ? -pr[r] : pr[r];
+        const int64_t x = x0 | M.rel(r << (4 * LAY));
+        z += ((x >> site) & 1) ? -pr[r] : pr[r];
       }
       z = wave_sum(z);
-      if (lane == 0) s_red[wave][1] = z;
-    } else {
-      for (int i = 0; i < A.L_real; ++i) {
-        double z = 0.0;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-          const int64_t x = gidx(tile_y(layout, t, r));
-          z += ((x >> i) & 1) ? -pr[r] : pr[r];
-        }
-        z = wave_sum(z);
-        if (lane == 0) s_red[wave][1 + i] = z;
-      }
+      if (lane == 0) s_red[wave][1 + i] = z;
     }
     __syncthreads();
     if (t < A.n_obs) {
@@ -301,46 +415,115 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
       A.partial[((int64_t)b * gridDim.x + tile) * A.n_obs + t] = acc;
     }
+  };
+  using IC2 = std::integral_constant<int, 2>;
+
+  // ---- pre-kick rounds: 2 -> 0 -> 1 ----
+  if constexpr (RP::pre) {
+    if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
+    if constexpr (RP::n0) {
+      exchange<2, 0>(v, s_tile, t);
+      apply_nibble<0, KIND>(v, s_pre, act);
+    }
+    if constexpr (RP::n1) {
+      exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
+      apply_nibble<1, KIND>(v, s_pre, act);
+    }
   }
-
-  double2* dst = A.dst + (int64_t)b * A.state_len;
+  // ---- diagonal and measurement at d_lay ----
+  using DL = std::integral_constant<int, RP::d_lay>;
+  if constexpr (RP::diag) diag_in(DL{});
+  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{});
+  // ---- post-kick rounds: 1 -> 0 -> 2 ----
+  if constexpr (RP::post) {
+    if constexpr (RP::n1) {
+      exchange<RP::d_lay, 1>(v, s_tile, t);
+      apply_nibble<1, KIND>(v, s_post, act);
+    }
+    if constexpr (RP::n0) {
+      exchange<RP::p1, 0>(v, s_tile, t);
+      apply_nibble<0, KIND>(v, s_post, act);
+    }
+    if constexpr (RP::n2) {
+      exchange<RP::p0, 2>(v, s_tile, t);
+      apply_nibble<2, KIND>(v, s_post, act);
+    }
+    exchange<RP::p2, 2>(v, s_tile, t);
+  } else {
+    exchange<RP::d_lay, 2>(v, s_tile, t);
+  }
+  if constexpr (!RP::diag) {
+    // no diagonal to carry the kicks' global phase
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) dst[gidx(tile_y(layout, t, r))] = v[r];
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
+  }
+  if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{});
+
+  char* dst = (char*)(A.dst + (int64_t)b * A.state_len);
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r)
+    *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
 }
 
-// Distinct kernel symbols per pass kind so rocprofv3 traces separate them.
-template <int MEAS>
-__global__ __launch_bounds__(kThreads, 2) void dtc_hi_pass(PassArgs A) {
-  pass_body<kDiagNone, MEAS>(A);
+// Kernel symbols per pass shape so rocprofv3 traces separate them.
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kdk_pass(PassArgs A) {
+  pass_body<kShapeKDK, NIBS, KIND>(A);
 }
-template <int MEAS>
-__global__ __launch_bounds__(kThreads, 2) void dtc_lo_pass_fwd(PassArgs A) {
-  pass_body<kDiagAfter, MEAS>(A);
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kd_pass(PassArgs A) {
+  pass_body<kShapeKD, NIBS, KIND>(A);
 }
-template <int MEAS>
-__global__ __launch_bounds__(kThreads, 2) void dtc_lo_pass_inv(PassArgs A) {
-  pass_body<kDiagBeforeConj, MEAS>(A);
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_dk_pass(PassArgs A) {
+  pass_body<kShapeDK, NIBS, KIND>(A);
+}
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kick_pass(PassArgs A) {
+  pass_body<kShapeK, NIBS, KIND>(A);
+}
+template <int NIBS>
+__global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
+  pass_body<kShapeD, NIBS, kKindRX>(A);
 }
 
-hipError_t launch_pass(const PassArgs& a, int batch, int diag_mode, int meas_mode,
-                       hipStream_t stream) {
-  const int n_tiles = 1 << (a.L_eff - kTileBits);
-  dim3 grid(n_tiles, batch), block(kThreads);
-#define DTC_LAUNCH(K, M) hipLaunchKernelGGL((K<M>), grid, block, 0, stream, a)
-  switch (diag_mode * 3 + meas_mode) {
-    case 0: DTC_LAUNCH(dtc_hi_pass, kMeasNone); break;
-    case 1: DTC_LAUNCH(dtc_hi_pass, kMeasProbe); break;
-    case 2: DTC_LAUNCH(dtc_hi_pass, kMeasSites); break;
-    case 3: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasNone); break;
-    case 4: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasProbe); break;
-    case 5: DTC_LAUNCH(dtc_lo_pass_fwd, kMeasSites); break;
-    case 6: DTC_LAUNCH(dtc_lo_pass_inv, kMeasNone); break;
-    case 7: DTC_LAUNCH(dtc_lo_pass_inv, kMeasProbe); break;
-    case 8: DTC_LAUNCH(dtc_lo_pass_inv, kMeasSites); break;
+template <int NIBS, int KIND>
+hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
+  dim3 block(kThreads);
+  switch (shape) {
+    case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
+    case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
+    case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
+    case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
+    case kShapeD: hipLaunchKernelGGL((dtc_diag_pass<NIBS>), grid, block, 0, stream, a); break;
     default: return hipErrorInvalidValue;
   }
-#undef DTC_LAUNCH
   return hipGetLastError();
+}
+
+template <int NIBS>
+hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, hipStream_t stream) {
+  switch (kind) {
+    case kKindRX: return launch_shape<NIBS, kKindRX>(a, grid, shape, stream);
+    case kKindRY: return launch_shape<NIBS, kKindRY>(a, grid, shape, stream);
+    case kKindGen: return launch_shape<NIBS, kKindGen>(a, grid, shape, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream) {
+  if (a.L_eff > 32 || a.L_eff < kTileBits) return hipErrorInvalidValue;
+  const int n_tiles = 1 << (a.L_eff - kTileBits);
+  dim3 grid(n_tiles, batch);
+  int nibs = 0;
+  for (int n = 0; n < 3; ++n)
+    if (a.act & (0xF << (4 * n))) nibs |= 1 << n;
+  switch (nibs) {
+    case 4: return launch_kind<4>(a, grid, shape, kind, stream);
+    case 6: return launch_kind<6>(a, grid, shape, kind, stream);
+    case 7: return launch_kind<7>(a, grid, shape, kind, stream);
+    default: return hipErrorInvalidValue;  // group layouts never produce other sets
+  }
 }
 
 __global__ void reduce_kernel(const double* __restrict__ partial, int n_tiles, int n_obs,
