@@ -36,7 +36,7 @@ def test_library_is_gfx950_code_object(pkg):
     assert ".hip_fatbin" in out.stdout
     blob = open(pkg._capi.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
-    assert b"dtc_lo_pass_fwd" in blob and b"dtc_hi_pass" in blob
+    assert b"dtc_kdk_pass" in blob and b"dtc_kick_pass" in blob
 
 
 def test_abi_version_and_null_errors(pkg):
