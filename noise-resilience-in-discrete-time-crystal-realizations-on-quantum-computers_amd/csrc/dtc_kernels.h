@@ -57,6 +57,8 @@ struct PassArgs {
   int tile_bits_mid;       // s - c  (tile-id bits deposited at [c, s))
   int act;                 // active tile-bit mask (sites kicked by this pass)
   // batch -> (instance, trajectory)
+  int batch;               // states in this launch
+  int persist_wgs;         // > 0: persistent launch with this many workgroups
   int64_t batch_start;
   int n_traj;
   int64_t traj_offset;

@@ -195,10 +195,12 @@ __device__ __forceinline__ double uni(double x) {
 
 template <int N, int KIND>
 __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const SiteMat* s_mat, int act) {
+  // Every site of an active nibble runs (inactive sites carry the identity):
+  // no data-dependent branches, so no register shuffles at merge points.
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int k = 4 * N + q;
-    if (act & (1 << k)) {
+    {
       // keep the scheduler from hoisting every layer's coefficient loads to
       // the top of the pass (register pressure -> spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -277,7 +279,7 @@ struct RoundPlan {
   static constexpr int p2 = n2 ? 2 : p0;
 };
 
-template <int SHAPE, int NIBS, int KIND>
+template <int SHAPE, int NIBS, int KIND, bool PERSIST>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
   __shared__ double2 s_tile[kTile];
@@ -289,207 +291,259 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double s_red[kThreads / 64][kMaxObs];
 
   const int t = threadIdx.x;
-  const int tile = blockIdx.x;
-  const int b = blockIdx.y;
-  const int64_t g = A.batch_start + b;
-  const int inst = (int)(g / A.n_traj);
-  const uint64_t traj = (uint64_t)(A.traj_offset + (g % A.n_traj));
   const int act = A.act;
   const int c = A.c, s = A.s;
+  const int tile_bits = A.L_eff - kTileBits;
+  const int64_t n_tiles = (int64_t)1 << tile_bits;
 
-  // tile base: tile-id bits deposited at [c, s) and [s + 12 - c, L_eff)
+  // work: tile indices idx = state * n_tiles + tile.  Non-persistent: one tile
+  // per workgroup.  Persistent: a contiguous range per workgroup (tiles of one
+  // state stay together, so kick matrices are rebuilt only when the state
+  // changes), with the next tile's loads in flight during this tile's rounds.
+  int64_t first, last;
+  if (PERSIST) {
+    const int64_t total = n_tiles * A.batch;
+    const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+    first = (int64_t)blockIdx.x * per;
+    last = first + per < total ? first + per : total;
+  } else {
+    first = (int64_t)blockIdx.y * n_tiles + blockIdx.x;
+    last = first + 1;
+  }
+  if (first >= last) return;
+
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
-  M.tbase = (((int64_t)tile & mid_mask) << c) |
-            (((int64_t)tile >> A.tile_bits_mid) << (s + kTileBits - c));
   M.c = c;
   M.s = s;
   M.cmask = (1 << c) - 1;
-
-  // Issue the tile loads first; the matrix / table setup below overlaps them.
-  // Address = uniform 64-bit base (tile base + register offset, SGPRs) + one
-  // per-lane 32-bit byte offset shared by all 16 loads (L_eff <= 32).
-  const char* src = (const char*)(A.src + (int64_t)b * A.state_len);
-  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
-  double2 v[kRegs];
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r)
-    v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
-
-  // kick matrices: threads 0..11 pre-kick, 64..75 post-kick (different waves);
-  // sites beyond L (padding of small systems) get the identity
-  if (t < 2 * kTileBits) s_k[t] = 0;
-  {
-    const bool is_pre = RP::pre && t < kTileBits;
-    const bool is_post = RP::post && t >= 64 && t < 64 + kTileBits;
-    const int k = is_pre ? t : t - 64;
-    if ((is_pre || is_post) && (act & (1 << k))) {
-      const KickDesc K = is_pre ? A.pre : A.post;
-      const int site = k < c ? k : s + k - c;
-      double2 m[4];
-      if (site < A.L_real) {
-        build_site_kick(A, K, site, traj, m);
-      } else {
-        m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
-        m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
-      }
-      SiteMat sm;
-      canonicalise(KIND, m, sm);
-      if (is_pre) s_pre[k] = sm;
-      else s_post[k] = sm;
-      atomicAdd(&s_k[0], sm.k);
-    }
-  }
-  // diagonal tables: chunk tables + the window table of the layout the
-  // diagonal is applied in (registers = 4 contiguous global bits [g0, g0+4))
-  int g0 = -1;
-  if (RP::diag) {
-    const int tb = 4 * RP::d_lay;
-    if (tb >= c) g0 = s + tb - c;
-    else if (tb + 4 <= c) g0 = tb;
-    const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
-    const double cs = A.diag_conj ? -1.0 : 1.0;
-    for (int i = t; i < A.n_chunks * 64; i += kThreads) {
-      const double2 e = dt[i];
-      s_chunk[i] = make_double2(e.x, cs * e.y);
-    }
-    if (g0 >= 0 && t < 64) {
-      const double2 e = dt[(A.n_chunks + g0) * 64 + t];
-      s_win[t] = make_double2(e.x, cs * e.y);
-    }
-  }
-  __syncthreads();  // matrices, phases and tables ready
-  // global phase i^k of the canonicalised kicks of this pass
-  const int kph = __builtin_amdgcn_readfirstlane(s_k[0]) & 3;
-  const double2 gph = make_double2(kph == 0 ? 1.0 : (kph == 2 ? -1.0 : 0.0),
-                                   kph == 1 ? 1.0 : (kph == 3 ? -1.0 : 0.0));
-
-  auto diag_in = [&](auto lay_tag) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int64_t x0 = M.at(ybase<LAY>(t));
-    if (g0 >= 0) {
-      // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
-      // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
-      // complex products per amplitude
-      const int w0i = (int)(((x0 << 1) >> g0) & 63);
-      const double2 w0 = s_win[w0i];
-      const double2 pc =
-          cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
-    } else {
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r)
-        v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
-                                               x0 | M.rel(r << (4 * LAY)))));
-    }
+  auto tile_base = [&](int64_t idx) -> int64_t {
+    const int64_t tile = idx & (n_tiles - 1);
+    return ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
   };
-  auto measure_in = [&](auto lay_tag) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int64_t x0 = M.at(ybase<LAY>(t));
-    const int wave = t >> 6, lane = t & 63;
-    double pr[kRegs];
-    double ptot = 0.0;
+  // Address = uniform 64-bit base (state + tile base + register offset, SGPRs)
+  // + one per-lane 32-bit byte offset shared by all 16 accesses (L_eff <= 32).
+  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
+  double2 vn[kRegs];
+  auto load_tile = [&](int64_t idx) {
+    const char* src = (const char*)(A.src + (idx >> tile_bits) * A.state_len);
+    const int64_t tb = tile_base(idx);
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
-      ptot += pr[r];
+    for (int r = 0; r < kRegs; ++r)
+      vn[r] = *(const double2*)(src + ((tb | M.rel(r << 8)) << 4) + vofs);
+  };
+  load_tile(first);
+
+  int64_t cur_state = -1;
+  double2 gph = make_double2(1.0, 0.0);
+  int g0 = -1;
+
+  for (int64_t idx = first; idx < last; ++idx) {
+    double2 v[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = vn[r];
+    if (PERSIST && idx + 1 < last) load_tile(idx + 1);
+    const int64_t b = idx >> tile_bits;
+    const int64_t tile = idx & (n_tiles - 1);
+    M.tbase = tile_base(idx);
+
+    if (b != cur_state) {
+      // ---- per-state setup: kick matrices (threads 0..11 pre, 64..75 post),
+      // their global phase, diagonal tables of the state's instance ----
+      cur_state = b;
+      const int64_t g = A.batch_start + b;
+      const int inst = (int)(g / A.n_traj);
+      const uint64_t traj = (uint64_t)(A.traj_offset + (g % A.n_traj));
+      if (PERSIST) __syncthreads();  // previous tile done with s_pre/s_post/tables
+      {
+        const bool is_pre = t < kTileBits;
+        const bool is_post = t >= 64 && t < 64 + kTileBits;
+        const int k = is_pre ? t : t - 64;
+        int kk = 0;
+        if ((is_pre && RP::pre) || (is_post && RP::post)) {
+          const KickDesc K = is_pre ? A.pre : A.post;
+          const int site = k < c ? k : s + k - c;
+          double2 m[4];
+          if ((act & (1 << k)) && site < A.L_real) {
+            build_site_kick(A, K, site, traj, m);
+          } else {  // inactive tile bits and padding sites: identity
+            m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
+            m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
+          }
+          SiteMat sm;
+          canonicalise(KIND, m, sm);
+          if (is_pre) s_pre[k] = sm;
+          else s_post[k] = sm;
+          kk = sm.k;
+        }
+        if (is_pre) s_k[k] = kk;
+        if (is_post) s_k[kTileBits + k] = kk;
+      }
+      // diagonal tables: chunk tables + the window table of the layout the
+      // diagonal is applied in (registers = 4 contiguous global bits [g0, g0+4))
+      if (RP::diag) {
+        const int tb = 4 * RP::d_lay;
+        g0 = tb >= c ? s + tb - c : (tb + 4 <= c ? tb : -1);
+        const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
+        const double cs = A.diag_conj ? -1.0 : 1.0;
+        for (int i = t; i < A.n_chunks * 64; i += kThreads) {
+          const double2 e = dt[i];
+          s_chunk[i] = make_double2(e.x, cs * e.y);
+        }
+        if (g0 >= 0 && t < 64) {
+          const double2 e = dt[(A.n_chunks + g0) * 64 + t];
+          s_win[t] = make_double2(e.x, cs * e.y);
+        }
+      }
+      __syncthreads();  // matrices, phases and tables ready
+      // global phase i^k of the canonicalised kicks of this pass
+      int ksum = 0;
+      for (int i = 0; i < 2 * kTileBits; ++i) ksum += s_k[i];
+      const int kph = __builtin_amdgcn_readfirstlane(ksum) & 3;
+      gph = make_double2(kph == 0 ? 1.0 : (kph == 2 ? -1.0 : 0.0),
+                         kph == 1 ? 1.0 : (kph == 3 ? -1.0 : 0.0));
     }
-    double tot = wave_sum(ptot);
-    if (lane == 0) s_red[wave][0] = tot;
-    const int n_z = A.meas == kMeasProbe ? 1 : A.L_real;
-    for (int i = 0; i < n_z; ++i) {
-      const int site = A.meas == kMeasProbe ? A.probe : i;
-      double z = 0.0;
+
+    auto diag_in = [&](auto lay_tag) {
+      constexpr int LAY = decltype(lay_tag)::value;
+      const int64_t x0 = M.at(ybase<LAY>(t));
+      if (g0 >= 0) {
+        // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
+        // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
+        // complex products per amplitude
+        const int w0i = (int)(((x0 << 1) >> g0) & 63);
+        const double2 w0 = s_win[w0i];
+        const double2 pc =
+            cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r)
+          v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
+                                                 x0 | M.rel(r << (4 * LAY)))));
+      }
+    };
+    auto measure_in = [&](auto lay_tag) {
+      constexpr int LAY = decltype(lay_tag)::value;
+      const int64_t x0 = M.at(ybase<LAY>(t));
+      const int wave = t >> 6, lane = t & 63;
+      double pr[kRegs];
+      double ptot = 0.0;
 #pragma unroll
       for (int r = 0; r < kRegs; ++r) {
-        const int64_t x = x0 | M.rel(r << (4 * LAY));
-        z += ((x >> site) & 1) ? -pr[r] : pr[r];
+        pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
+        ptot += pr[r];
       }
-      z = wave_sum(z);
-      if (lane == 0) s_red[wave][1 + i] = z;
-    }
-    __syncthreads();
-    if (t < A.n_obs) {
-      double acc = 0.0;
-      for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
-      A.partial[((int64_t)b * gridDim.x + tile) * A.n_obs + t] = acc;
-    }
-  };
-  using IC2 = std::integral_constant<int, 2>;
-
-  // ---- pre-kick rounds: 2 -> 0 -> 1 ----
-  if constexpr (RP::pre) {
-    if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
-    if constexpr (RP::n0) {
-      exchange<2, 0>(v, s_tile, t);
-      apply_nibble<0, KIND>(v, s_pre, act);
-    }
-    if constexpr (RP::n1) {
-      exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
-      apply_nibble<1, KIND>(v, s_pre, act);
-    }
-  }
-  // ---- diagonal and measurement at d_lay ----
-  using DL = std::integral_constant<int, RP::d_lay>;
-  if constexpr (RP::diag) diag_in(DL{});
-  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{});
-  // ---- post-kick rounds: 1 -> 0 -> 2 ----
-  if constexpr (RP::post) {
-    if constexpr (RP::n1) {
-      exchange<RP::d_lay, 1>(v, s_tile, t);
-      apply_nibble<1, KIND>(v, s_post, act);
-    }
-    if constexpr (RP::n0) {
-      exchange<RP::p1, 0>(v, s_tile, t);
-      apply_nibble<0, KIND>(v, s_post, act);
-    }
-    if constexpr (RP::n2) {
-      exchange<RP::p0, 2>(v, s_tile, t);
-      apply_nibble<2, KIND>(v, s_post, act);
-    }
-    exchange<RP::p2, 2>(v, s_tile, t);
-  } else {
-    exchange<RP::d_lay, 2>(v, s_tile, t);
-  }
-  if constexpr (!RP::diag) {
-    // no diagonal to carry the kicks' global phase
+      double tot = wave_sum(ptot);
+      if (PERSIST) __syncthreads();  // s_red of the previous tile consumed
+      if (lane == 0) s_red[wave][0] = tot;
+      const int n_z = A.meas == kMeasProbe ? 1 : A.L_real;
+      for (int i = 0; i < n_z; ++i) {
+        const int site = A.meas == kMeasProbe ? A.probe : i;
+        double z = 0.0;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
-  }
-  if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{});
+        for (int r = 0; r < kRegs; ++r) {
+          const int64_t x = x0 | M.rel(r << (4 * LAY));
+          z += ((x >> site) & 1) ? -pr[r] : pr[r];
+        }
+        z = wave_sum(z);
+        if (lane == 0) s_red[wave][1 + i] = z;
+      }
+      __syncthreads();
+      if (t < A.n_obs) {
+        double acc = 0.0;
+        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
+        A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+      }
+    };
+    using IC2 = std::integral_constant<int, 2>;
 
-  char* dst = (char*)(A.dst + (int64_t)b * A.state_len);
+    // ---- pre-kick rounds: 2 -> 0 -> 1 ----
+    if constexpr (RP::pre) {
+      if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
+      if constexpr (RP::n0) {
+        exchange<2, 0>(v, s_tile, t);
+        apply_nibble<0, KIND>(v, s_pre, act);
+      }
+      if constexpr (RP::n1) {
+        exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
+        apply_nibble<1, KIND>(v, s_pre, act);
+      }
+    }
+    // ---- diagonal and measurement at d_lay ----
+    using DL = std::integral_constant<int, RP::d_lay>;
+    if constexpr (RP::diag) diag_in(DL{});
+    if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{});
+    // ---- post-kick rounds: 1 -> 0 -> 2 ----
+    if constexpr (RP::post) {
+      if constexpr (RP::n1) {
+        exchange<RP::d_lay, 1>(v, s_tile, t);
+        apply_nibble<1, KIND>(v, s_post, act);
+      }
+      if constexpr (RP::n0) {
+        exchange<RP::p1, 0>(v, s_tile, t);
+        apply_nibble<0, KIND>(v, s_post, act);
+      }
+      if constexpr (RP::n2) {
+        exchange<RP::p0, 2>(v, s_tile, t);
+        apply_nibble<2, KIND>(v, s_post, act);
+      }
+      exchange<RP::p2, 2>(v, s_tile, t);
+    } else {
+      exchange<RP::d_lay, 2>(v, s_tile, t);
+    }
+    if constexpr (!RP::diag) {
+      // no diagonal to carry the kicks' global phase
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r)
-    *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
+    }
+    if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{});
+
+    char* dst = (char*)(A.dst + b * A.state_len);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r)
+      *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+  }
 }
 
-// Kernel symbols per pass shape so rocprofv3 traces separate them.
-template <int NIBS, int KIND>
-__global__ __launch_bounds__(kThreads, 2) void dtc_kdk_pass(PassArgs A) {
-  pass_body<kShapeKDK, NIBS, KIND>(A);
-}
-template <int NIBS, int KIND>
-__global__ __launch_bounds__(kThreads, 2) void dtc_kd_pass(PassArgs A) {
-  pass_body<kShapeKD, NIBS, KIND>(A);
-}
-template <int NIBS, int KIND>
-__global__ __launch_bounds__(kThreads, 2) void dtc_dk_pass(PassArgs A) {
-  pass_body<kShapeDK, NIBS, KIND>(A);
-}
-template <int NIBS, int KIND>
-__global__ __launch_bounds__(kThreads, 2) void dtc_kick_pass(PassArgs A) {
-  pass_body<kShapeK, NIBS, KIND>(A);
-}
+// Kernel symbols per pass shape so rocprofv3 traces separate them.  The
+// persistent variants (1 workgroup per CU, next tile prefetched into
+// registers) carry a _p suffix.
+#define DTC_DEFINE_PASS(NAME, SHAPE_EXPR)                                          \
+  template <int NIBS, int KIND>                                                    \
+  __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
+    pass_body<SHAPE_EXPR, NIBS, KIND, false>(A);                                   \
+  }                                                                                \
+  template <int NIBS, int KIND>                                                    \
+  __global__ __launch_bounds__(kThreads, 1) void NAME##_p(PassArgs A) {            \
+    pass_body<SHAPE_EXPR, NIBS, KIND, true>(A);                                    \
+  }
+DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
+DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
+DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
+DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
+#undef DTC_DEFINE_PASS
 template <int NIBS>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
-  pass_body<kShapeD, NIBS, kKindRX>(A);
+  pass_body<kShapeD, NIBS, kKindRX, false>(A);
 }
 
 template <int NIBS, int KIND>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
+  if (a.persist_wgs > 0) {
+    dim3 pg(a.persist_wgs);
+    switch (shape) {
+      case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
+      case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
+      case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
+      case kShapeK: hipLaunchKernelGGL((dtc_kick_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
+      case kShapeD: hipLaunchKernelGGL((dtc_diag_pass<NIBS>), grid, block, 0, stream, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (shape) {
     case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
     case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
@@ -512,7 +566,7 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, hipStr
 }
 
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream) {
-  if (a.L_eff > 32 || a.L_eff < kTileBits) return hipErrorInvalidValue;
+  if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch) return hipErrorInvalidValue;
   const int n_tiles = 1 << (a.L_eff - kTileBits);
   dim3 grid(n_tiles, batch);
   int nibs = 0;
