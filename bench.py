@@ -16,8 +16,8 @@ keyed by global trajectory id), and the per-t sums are all-reduced once at
 the end over RCCL.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-"roofline" for the fused RZZ+RZ diagonal + low-site kick kernel (HIP events
-on the engine's stream over the timed region) and "cpu_baseline" = the C
+"roofline" for the K-D-K pass kernel (kick . RZZ/RZ diagonal . kick; HIP events
+on the engine's stream over the timed region, all passes that apply the diagonal) and "cpu_baseline" = the C
 oracle (oracle/dtc_oracle.c) on this host's cores for a bounded sample.
 """
 from __future__ import annotations
@@ -210,7 +210,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "pass_kernel<diag> (fused RZZ+RZ diagonal + sites 0..11 kick)",
+            "kernel": ("dtc_kdk_pass (kick layer . fused RZZ+RZ diagonal . kick layer; one "
+                       "launch advances every state by one Floquet period)"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -223,9 +224,9 @@ def main():
             "launches": lo["launches"],
         },
         "kernels": {
-            "lo_pass": {"launches": lo["launches"], "avg_ms": avg_lo * 1e3,
+            "kdk_pass": {"launches": lo["launches"], "avg_ms": avg_lo * 1e3,
                         "GBps": launch_bytes / avg_lo / 1e9 if lo["launches"] else None},
-            "hi_pass": {"launches": hi["launches"], "avg_ms": avg_hi * 1e3,
+            "kick_pass": {"launches": hi["launches"], "avg_ms": avg_hi * 1e3,
                         "GBps": launch_bytes / avg_hi / 1e9 if hi["launches"] else None},
             "reduce": {"launches": stats[2]["launches"], "total_ms": stats[2]["total_ms"]},
             "kernel_time_frac": (lo["total_ms"] + hi["total_ms"] + stats[2]["total_ms"])
