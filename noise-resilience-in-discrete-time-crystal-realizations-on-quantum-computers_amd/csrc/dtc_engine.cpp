@@ -631,7 +631,11 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   if (B <= 0) {
     size_t free_b = 0, total_b = 0;
     DTC_HIP(hipMemGetInfo(&free_b, &total_b));
-    double budget = std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
+    // small states: ~64 GiB of batch saturates the device; large states
+    // (L >= 24, C4-style instance batches) may use most of the 288 GB
+    double budget = per_state >= (double)(256ull << 20)
+                        ? 0.7 * (double)free_b
+                        : std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
     if (const char* env = std::getenv("DTC_BATCH_BYTES")) budget = std::atof(env);
     B = (int64_t)(budget / per_state);
     B = std::max<int64_t>(1, std::min<int64_t>(B, 4096));

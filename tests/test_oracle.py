@@ -202,3 +202,26 @@ def test_c_oracle_apply_periods_inverse_roundtrip(pkg):
     b, z = c_oracle.apply_periods(spec, a, 5, 5, inverse=True)
     np.testing.assert_allclose(b, psi, atol=1e-12)
     assert abs(z[0] - 1) < 1e-12
+
+
+def test_blocks_factorise_oracle(pkg):
+    """The property tests/test_gpu_large.py relies on at L=28, checked with the
+    oracle at L=10: zero couplings on two bonds split the chain, and per-site
+    <Z_i(t)> of the full chain equal those of the block holding i."""
+    rng = np.random.default_rng(10)
+    L, T, g, cuts = 10, 8, 0.93, (3, 6)
+    hs = rng.uniform(-np.pi, np.pi, (1, L))
+    phis = rng.uniform(-1.5 * np.pi, -0.5 * np.pi, (1, L - 1))
+    phis[:, list(cuts)] = 0.0
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, polarization="circular_left",
+                         initial_state="neel", use_noise=0)
+    full = c_oracle.autocorr(spec, 1, want_echo=False, want_zsite=True)["zsite"]
+    mask, lo = spec.init_mask, 0
+    for hi in (cuts[0] + 1, cuts[1] + 1, L):
+        Lb = hi - lo
+        b = pkg.SweepSpec(L=Lb, T=T, hs=hs[:, lo:hi], phis=phis[:, lo:hi - 1], g=g,
+                          use_noise=0, kick=spec.kick[:, lo:hi],
+                          init_mask_value=(mask >> lo) & ((1 << Lb) - 1))
+        ref = c_oracle.autocorr(b, 1, want_echo=False, want_zsite=True)["zsite"]
+        assert np.abs(full[..., lo:hi] - ref).max() < 1e-12
+        lo = hi
