@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 1
+#define DTC_ABI_VERSION 2
 
 /* error codes */
 #define DTC_OK 0
@@ -119,6 +119,51 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* no
                       uint64_t seed, int32_t inst, int64_t traj, uint32_t stream,
                       int32_t first_period, int32_t n_periods, int32_t inverse,
                       double* state, double* zsite_out);
+
+/* ---- One state sharded over ranks (L=34 over 8 GPUs).
+ * The 2^L amplitudes are split over 2^n_global ranks; a shard holds 2^n_local
+ * amplitudes (n_local = L - n_global, 12 <= n_local <= 32).  Physical index bit
+ * q < n_local of a shard holds logical site site_of[q]; bit k of the rank id
+ * holds site site_of[n_local + k].  A call may hold n_shards consecutive ranks
+ * (first_rank ..) whose shards lie 2^n_local amplitudes apart in one device
+ * buffer ("virtual ranks": one GPU emulating several; 1 per process on a
+ * multi-GPU node).  Every logical bond whose two sites are both local must join
+ * physically adjacent bits.  The kick on a global site is applied after the
+ * caller's all-to-all exchange has made it local (the sweep driver alternates
+ * two bit maps, see sharded.py); the RZZ/RZ diagonal never needs one: bonds and
+ * fields on rank bits become per-rank effective fields and a per-rank phase.
+ * Replaces the reference's whole-state Aer run of a circuit too large for one
+ * device; there is no reference call site for it (fast.py caps L at 20). */
+typedef struct dtc_shard {
+  int32_t n_local;
+  int32_t n_global;
+  int32_t n_shards;
+  int32_t first_rank;
+  int32_t site_of[64];
+} dtc_shard;
+
+/* state (device pointer, n_shards * 2^n_local complex128): the Z-basis product
+ * state prob->init_mask of trajectory traj (noisy X preparation, fast.py:127-130,
+ * drawn as in dtc_autocorr), distributed per site_of. */
+int dtc_shard_set_basis(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                        const dtc_shard* shard, uint64_t seed, int64_t traj, double* state);
+
+/* One step on every shard held (device pointers; src may equal dst):
+ *   dst = K_{period+1}[post_mask] . D^diag . K_period[pre_mask] . src
+ * where K_p[mask] = the period-p kick (fast.py:113, forward RNG stream 0, RNG
+ * period counter p, trajectory traj) on the logical sites at the physical
+ * local bits in mask, and D = the RZZ+RZ layer (fast.py:115-120) of instance
+ * inst.  obs (host, nullable): [n_shards][1 + n_local] = (sum |a|^2,
+ * sum z_q |a|^2 per physical bit q) of each shard after D (at the end when
+ * diag = 0).  Synchronous. */
+int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                   const dtc_shard* shard, uint64_t seed, int64_t traj, int32_t inst,
+                   int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                   const double* src, double* dst, double* obs);
+
+/* Host-only: the site groups the engine's passes use for an n_bits-bit state
+ * (bit masks, one per group; returns the count or a negative error). */
+int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups);
 
 /* Profiling: when enabled, every kernel launch is bracketed by HIP events on
  * the ctx stream and accumulated per kernel kind. */

@@ -27,6 +27,9 @@ EXPORTED_SYMBOLS = (
     "dtc_kernel_stats",
     "dtc_reset_stats",
     "dtc_device_info",
+    "dtc_shard_set_basis",
+    "dtc_shard_step",
+    "dtc_plan_groups",
 )
 
 KERNEL_LO_PASS = 0
@@ -74,6 +77,18 @@ class DtcNoise(ctypes.Structure):
     ]
 
 
+class DtcShard(ctypes.Structure):
+    """Mirror of ``dtc_shard`` (include/dtc.h)."""
+
+    _fields_ = [
+        ("n_local", ctypes.c_int32),
+        ("n_global", ctypes.c_int32),
+        ("n_shards", ctypes.c_int32),
+        ("first_rank", ctypes.c_int32),
+        ("site_of", ctypes.c_int32 * 64),
+    ]
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -117,6 +132,16 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         lib.dtc_device_info.argtypes = [
             ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, P(ctypes.c_int32), _dp,
         ]
+        lib.dtc_shard_set_basis.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_void_p,
+        ]
+        lib.dtc_shard_step.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
+            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, _dp,
+        ]
+        lib.dtc_plan_groups.argtypes = [ctypes.c_int32, P(ctypes.c_uint64), ctypes.c_int32]
         for name in EXPORTED_SYMBOLS:
             if name not in ("dtc_last_error", "dtc_abi_version"):
                 getattr(lib, name).restype = ctypes.c_int
@@ -135,3 +160,13 @@ def as_dptr(a: np.ndarray | None):
         return None
     assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(_dp)
+
+
+def plan_groups(n_bits: int) -> list:
+    """Host-only: bit masks of the site groups the engine's passes use."""
+    lib = load_library()
+    buf = (ctypes.c_uint64 * 16)()
+    n = lib.dtc_plan_groups(int(n_bits), buf, 16)
+    if n < 0:
+        check(n)
+    return [int(buf[i]) for i in range(n)]

@@ -74,7 +74,7 @@ struct Pending {
 struct dtc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis;
+  DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
   bool prof = false;
   int persist_wgs = 0;  // persistent pass kernels: workgroups per launch (0 = off)
   int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
@@ -195,7 +195,7 @@ double diag_angle(int L, const double* hh, const double* pp, int lo_site, int hi
 }
 
 void build_diag_tables(const Plan& pl, int n_inst, const double* h, const double* phi,
-                       std::vector<double>& out) {
+                       std::vector<double>& out, const double* const_angle = nullptr) {
   const int L = pl.L;
   out.assign((size_t)n_inst * pl.diag_stride * 2, 0.0);
   for (int in = 0; in < n_inst; ++in) {
@@ -208,9 +208,10 @@ void build_diag_tables(const Plan& pl, int n_inst, const double* h, const double
     };
     for (int k = 0; k < pl.n_chunks; ++k) {
       const int b0 = dtc::kChunkBits * k;
+      const double c0 = (k == 0 && const_angle) ? const_angle[in] : 0.0;
       for (int v = 0; v < 64; ++v)
-        put(k * 64 + v, diag_angle(L, hh, pp, b0, b0 + dtc::kChunkBits, b0,
-                                   b0 + dtc::kChunkBits, b0, v));
+        put(k * 64 + v, c0 + diag_angle(L, hh, pp, b0, b0 + dtc::kChunkBits, b0,
+                                        b0 + dtc::kChunkBits, b0, v));
     }
     for (int g0 = 0; g0 < pl.L_eff; ++g0) {
       for (int v = 0; v < 64; ++v) {
@@ -231,6 +232,7 @@ struct RunCfg {
   int n_traj;
   int noisy;
   uint32_t thr1, thr2, thr3;
+  const int* site_of = nullptr;  // device: physical bit -> logical site (shards)
 };
 
 // ---- layer chains ---------------------------------------------------------
@@ -283,6 +285,8 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.state_len = rc.pl.len;
   A.L_eff = rc.pl.L_eff;
   A.L_real = rc.pl.L;
+  A.L_kick = rc.prob->L;
+  A.site_of = rc.site_of;
   A.batch_start = batch_start;
   A.n_traj = rc.n_traj;
   A.traj_offset = rc.traj_offset;
@@ -435,9 +439,11 @@ int run_chain(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch, Ch
   return DTC_OK;
 }
 
-int check_problem(const dtc_problem* pr, const dtc_noise* nz) {
+int check_problem(const dtc_problem* pr, const dtc_noise* nz, int max_L = 32) {
   if (!pr || !nz) return fail(DTC_EINVAL, "null problem/noise");
-  if (pr->L < 1 || pr->L > 32) return fail(DTC_EINVAL, "L must be in [1, 32] per device");
+  if (pr->L < 1 || pr->L > max_L)
+    return fail(DTC_EINVAL, max_L == 32 ? "L must be in [1, 32] per device (larger: dtc_shard_*)"
+                                        : "L out of range");
   if (pr->T < 1) return fail(DTC_EINVAL, "T must be >= 1");
   if (pr->n_inst < 1) return fail(DTC_EINVAL, "n_inst must be >= 1");
   if (pr->probe_site < 0 || pr->probe_site >= pr->L)
@@ -493,6 +499,77 @@ int upload_tables(dtc_ctx* ctx, const dtc_problem* pr, const Plan& pl) {
   return DTC_OK;
 }
 
+
+// ---- sharded state (include/dtc.h: dtc_shard) ---------------------------------
+
+int check_shard(const dtc_problem* pr, const dtc_shard* sh) {
+  if (!sh) return fail(DTC_EINVAL, "null shard");
+  const int L = pr->L, nl = sh->n_local, ng = sh->n_global;
+  if (ng < 0 || ng > 16 || nl + ng != L) return fail(DTC_EINVAL, "n_local + n_global must equal L");
+  if (nl < dtc::kTileBits || nl > 32) return fail(DTC_EINVAL, "n_local must be in [12, 32]");
+  if (sh->n_shards < 1 || sh->first_rank < 0 ||
+      (int64_t)sh->first_rank + sh->n_shards > ((int64_t)1 << ng))
+    return fail(DTC_EINVAL, "shard ranks outside [0, 2^n_global)");
+  std::vector<int> seen(L, 0);
+  for (int q = 0; q < L; ++q) {
+    const int v = sh->site_of[q];
+    if (v < 0 || v >= L || seen[v]++) return fail(DTC_EINVAL, "site_of is not a permutation");
+  }
+  // every bond between two local sites must join adjacent physical bits
+  std::vector<int> bit_of(L);
+  for (int q = 0; q < L; ++q) bit_of[sh->site_of[q]] = q;
+  for (int i = 0; i + 1 < L; ++i) {
+    const int a = bit_of[i], b = bit_of[i + 1];
+    if (a < nl && b < nl && std::abs(a - b) != 1)
+      return fail(DTC_EINVAL, "a bond between two local sites is not physically adjacent");
+  }
+  return DTC_OK;
+}
+
+// Effective chain of one shard: local fields/bonds over physical bits plus the
+// constant angle of the rank's global sites (fields, bonds to and among them).
+void shard_chain(const dtc_problem* pr, const dtc_shard* sh, int inst, int rank,
+                 double* h_eff, double* phi_eff, double* c_angle) {
+  const int L = pr->L, nl = sh->n_local;
+  const double* h = pr->h + (size_t)inst * L;
+  const double* phi = pr->phi + (size_t)inst * (L > 1 ? L - 1 : 0);
+  std::vector<int> bit_of(L);
+  for (int q = 0; q < L; ++q) bit_of[sh->site_of[q]] = q;
+  auto zg = [&](int site) {  // z of a global site on this rank
+    return ((rank >> (bit_of[site] - nl)) & 1) ? -1.0 : 1.0;
+  };
+  double c = 0.0;
+  for (int q = 0; q < nl; ++q) h_eff[q] = h[sh->site_of[q]];
+  for (int q = 0; q + 1 < nl; ++q) phi_eff[q] = 0.0;
+  for (int i = 0; i < L; ++i)
+    if (bit_of[i] >= nl) c += h[i] * zg(i);
+  for (int i = 0; i + 1 < L; ++i) {
+    const int a = bit_of[i], b = bit_of[i + 1];
+    if (a < nl && b < nl) phi_eff[std::min(a, b)] = phi[i];
+    else if (a < nl) h_eff[a] += phi[i] * zg(i + 1);
+    else if (b < nl) h_eff[b] += phi[i] * zg(i);
+    else c += phi[i] * zg(i) * zg(i + 1);
+  }
+  *c_angle = c;
+}
+
+uint64_t group_bits(const Group& g) {
+  uint64_t m = 0;
+  for (int k = 0; k < dtc::kTileBits; ++k)
+    if (g.act & (1 << k)) m |= 1ull << (k < g.c ? k : g.s + k - g.c);
+  return m;
+}
+
+// tile bits of group g that are NOT in mask (left identity by a kick layer)
+uint32_t skip_bits(const Group& g, uint64_t mask) {
+  uint32_t sk = 0;
+  for (int k = 0; k < dtc::kTileBits; ++k) {
+    if (!(g.act & (1 << k))) continue;
+    const int bit = k < g.c ? k : g.s + k - g.c;
+    if (!((mask >> bit) & 1)) sk |= 1u << k;
+  }
+  return sk;
+}
 }  // namespace
 
 extern "C" {
@@ -547,6 +624,7 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->diag);
   release(ctx->kick);
   release(ctx->basis);
+  release(ctx->sitemap);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return DTC_OK;
@@ -794,6 +872,166 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
     }
     for (int i = 0; i <= L; ++i) zsite_out[i] = acc[i];
   }
+  return DTC_OK;
+}
+
+
+int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups) {
+  if (n_bits < 1 || n_bits > 40 || !masks) return fail(DTC_EINVAL, "bad arguments");
+  Plan pl = make_plan(n_bits);
+  if ((int)pl.groups.size() > max_groups) return fail(DTC_EINVAL, "max_groups too small");
+  for (size_t g = 0; g < pl.groups.size(); ++g)
+    masks[g] = group_bits(pl.groups[g]) & ((n_bits >= 64) ? ~0ull : ((1ull << n_bits) - 1));
+  return (int32_t)pl.groups.size();
+}
+
+int dtc_shard_set_basis(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                        const dtc_shard* sh, uint64_t seed, int64_t traj, double* state) {
+  if (!ctx || !state) return fail(DTC_EINVAL, "null ctx/state");
+  DTC_TRY(check_problem(pr, nz, 64));
+  DTC_TRY(check_shard(pr, sh));
+  if (traj < 0) return fail(DTC_EINVAL, "traj must be >= 0");
+  DTC_HIP(hipSetDevice(ctx->device));
+  uint64_t mask = pr->init_mask;
+  if (nz->p > 0.0) {  // as init_state_mask: X/Y errors after a prep X undo the flip
+    uint32_t t1, t2, t3;
+    thresholds(nz->p, &t1, &t2, &t3);
+    for (int i = 0; i < pr->L; ++i) {
+      if (!((pr->init_mask >> i) & 1ull)) continue;
+      const int pz = dtc::sample_pauli(seed, (uint64_t)traj, dtc::kStreamPrep, 0u, (uint32_t)i,
+                                       0u, t1, t2, t3);
+      if (pz == 1 || pz == 2) mask &= ~(1ull << i);
+    }
+  }
+  const int nl = sh->n_local;
+  const size_t len = (size_t)1 << nl;
+  DTC_HIP(hipMemsetAsync(state, 0, len * 16 * sh->n_shards, ctx->stream));
+  uint64_t local = 0, rank = 0;
+  for (int q = 0; q < pr->L; ++q) {
+    const uint64_t bit = (mask >> sh->site_of[q]) & 1;
+    if (q < nl) local |= bit << q;
+    else rank |= bit << (q - nl);
+  }
+  const int64_t b = (int64_t)rank - sh->first_rank;
+  static const double one[2] = {1.0, 0.0};
+  if (b >= 0 && b < sh->n_shards)
+    DTC_HIP(hipMemcpyAsync(state + 2 * ((size_t)b * len + local), one, 16,
+                           hipMemcpyHostToDevice, ctx->stream));
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  return DTC_OK;
+}
+
+int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                   const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t inst,
+                   int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                   const double* src, double* dst, double* obs) {
+  if (!ctx || !src || !dst) return fail(DTC_EINVAL, "null ctx/src/dst");
+  DTC_TRY(check_problem(pr, nz, 64));
+  DTC_TRY(check_shard(pr, sh));
+  if (inst < 0 || inst >= pr->n_inst) return fail(DTC_EINVAL, "inst out of range");
+  if (traj < 0) return fail(DTC_EINVAL, "traj must be >= 0");
+  const int nl = sh->n_local;
+  const uint64_t all = nl >= 64 ? ~0ull : (1ull << nl) - 1;
+  if ((pre_mask | post_mask) & ~all) return fail(DTC_EINVAL, "kick mask has non-local bits");
+  if (post_mask && !diag) return fail(DTC_EINVAL, "post_mask needs diag");
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  if (pre_mask && (period < 1 || period > n_rows))
+    return fail(DTC_EINVAL, "period outside kick table");
+  if (post_mask && period + 1 > n_rows) return fail(DTC_EINVAL, "period + 1 outside kick table");
+  DTC_HIP(hipSetDevice(ctx->device));
+
+  RunCfg rc;
+  rc.prob = pr;
+  rc.pl = make_plan(nl);
+  rc.seed = seed;
+  rc.traj_offset = traj;
+  rc.n_traj = 1;  // batch index b = shard b -> diag table b
+  rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
+  thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  const Plan& pl = rc.pl;
+  const int B = sh->n_shards;
+
+  // tables: per-shard effective diagonal, logical kick table, bit -> site map
+  std::vector<double> he((size_t)B * nl), pe((size_t)B * std::max(nl - 1, 1)), ca(B);
+  for (int b = 0; b < B; ++b)
+    shard_chain(pr, sh, inst, sh->first_rank + b, he.data() + (size_t)b * nl,
+                pe.data() + (size_t)b * std::max(nl - 1, 1), &ca[b]);
+  std::vector<double> dt;
+  build_diag_tables(pl, B, he.data(), pe.data(), dt, ca.data());
+  DTC_TRY(ensure(ctx->diag, dt.size() * sizeof(double)));
+  DTC_HIP(hipMemcpyAsync(ctx->diag.p, dt.data(), dt.size() * sizeof(double),
+                         hipMemcpyHostToDevice, ctx->stream));
+  const size_t kb = (size_t)n_rows * pr->L * pr->n_sub * 8 * sizeof(double);
+  DTC_TRY(ensure(ctx->kick, kb));
+  DTC_HIP(hipMemcpyAsync(ctx->kick.p, pr->kick, kb, hipMemcpyHostToDevice, ctx->stream));
+  DTC_TRY(ensure(ctx->sitemap, 64 * sizeof(int)));
+  DTC_HIP(hipMemcpyAsync(ctx->sitemap.p, sh->site_of, 64 * sizeof(int), hipMemcpyHostToDevice,
+                         ctx->stream));
+  rc.site_of = (const int*)ctx->sitemap.p;
+  const int n_obs = 1 + nl;
+  DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
+  DTC_TRY(ensure(ctx->vals_f, (size_t)B * n_obs * sizeof(double)));
+
+  auto layer = [&](int p, uint64_t mask, const Group& g) {
+    dtc::KickDesc k{1, p - 1, dtc::kKickForward, dtc::kStreamForward, (uint32_t)p,
+                    skip_bits(g, mask)};
+    return k;
+  };
+  // main group: holds the highest kicked bit (the bits an exchange just made local)
+  const uint64_t any = pre_mask | post_mask;
+  int main_g = (int)pl.groups.size() - 1;
+  if (any) {
+    const int top = 63 - __builtin_clzll(any);
+    for (size_t g = 0; g < pl.groups.size(); ++g)
+      if ((group_bits(pl.groups[g]) >> top) & 1) main_g = (int)g;
+  }
+  std::vector<PassSpec> passes;
+  for (size_t g = 0; g < pl.groups.size(); ++g) {
+    const uint64_t gb = group_bits(pl.groups[g]);
+    if ((int)g != main_g && (pre_mask & gb))
+      passes.push_back(PassSpec{(int)g, layer(period, pre_mask, pl.groups[g]), no_kick(),
+                                dtc::kDiagNone, 0});
+  }
+  const Group& mg = pl.groups[main_g];
+  const uint64_t mb = group_bits(mg);
+  PassSpec mp{main_g, no_kick(), no_kick(), diag ? dtc::kDiagFwd : dtc::kDiagNone, 1};
+  if (pre_mask & mb) mp.pre = layer(period, pre_mask, mg);
+  if (post_mask & mb) mp.post = layer(period + 1, post_mask, mg);
+  const int main_idx = (int)passes.size();
+  if (mp.pre.enabled || mp.post.enabled || diag) passes.push_back(mp);
+  const int meas_idx = diag ? main_idx : (int)passes.size() - 1;
+  for (size_t g = 0; g < pl.groups.size(); ++g) {
+    const uint64_t gb = group_bits(pl.groups[g]);
+    if ((int)g != main_g && (post_mask & gb))
+      passes.push_back(PassSpec{(int)g, layer(period + 1, post_mask, pl.groups[g]), no_kick(),
+                                dtc::kDiagNone, 0});
+  }
+  const double2* s2 = (const double2*)src;
+  double2* d2 = (double2*)dst;
+  const size_t len = (size_t)1 << nl;
+  if (passes.empty()) {
+    if (src != dst)
+      DTC_HIP(hipMemcpyAsync(d2, s2, len * 16 * B, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  for (size_t i = 0; i < passes.size(); ++i) {
+    const bool meas = obs && (int)i == meas_idx;
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, B, passes[i], i == 0 ? s2 : d2, d2,
+                             meas ? dtc::kMeasSites : dtc::kMeasNone, diag ? 0 : 1, n_obs,
+                             meas ? (double*)ctx->vals_f.p : nullptr, n_obs));
+  }
+  if (obs && passes.empty()) {
+    // no pass ran: measure with an identity-only kick pass over group 0
+    PassSpec ps{0, layer(1, 0, pl.groups[0]), no_kick(), dtc::kDiagNone, 0};
+    ps.pre.row = 0;
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, B, ps, d2, d2, dtc::kMeasSites, 1, n_obs,
+                             (double*)ctx->vals_f.p, n_obs));
+  }
+  if (obs)
+    DTC_HIP(hipMemcpyAsync(obs, ctx->vals_f.p, (size_t)B * n_obs * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->prof) DTC_TRY(resolve_pending(ctx));
   return DTC_OK;
 }
 

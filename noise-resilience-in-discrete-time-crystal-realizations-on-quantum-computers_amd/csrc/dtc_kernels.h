@@ -38,6 +38,7 @@ struct KickDesc {
   int mode;             // KickMode
   uint32_t stream;      // RNG stream (0 forward, 1 + t echo branch at t)
   uint32_t rng_period;  // RNG period counter
+  uint32_t skip;        // tile bits of the pass left unkicked (identity); 0 = none
 };
 
 // One streaming pass over a batch of states.  A tile covers index bits
@@ -63,8 +64,10 @@ struct PassArgs {
   int n_traj;
   int64_t traj_offset;
   // kicks
-  const double2* kick;     // [n_periods][L_real][n_sub][4]
+  const double2* kick;     // [n_periods][L_kick][n_sub][4]
   int n_sub;
+  int L_kick;              // sites per kick-table row (logical chain length)
+  const int* site_of;      // physical index bit -> logical site (sharded states); null = identity
   KickDesc pre, post;
   // noise
   uint32_t thr1, thr2, thr3;

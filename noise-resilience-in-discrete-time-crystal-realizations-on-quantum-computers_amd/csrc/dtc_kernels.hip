@@ -117,9 +117,10 @@ __device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, 
   m[2] = make_double2(0.0, 0.0);
   m[3] = make_double2(1.0, 0.0);
   const bool inv = (K.mode == kKickInverse);
+  if (A.site_of) site = A.site_of[site];  // sharded state: physical bit -> logical site
   for (int q = 0; q < A.n_sub; ++q) {
     const int qq = inv ? (A.n_sub - 1 - q) : q;
-    const double2* gp = A.kick + (((int64_t)K.row * A.L_real + site) * A.n_sub + qq) * 4;
+    const double2* gp = A.kick + (((int64_t)K.row * A.L_kick + site) * A.n_sub + qq) * 4;
     double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
     if (inv) dagger(gm);
     mat_mul(m, gm, m);
@@ -364,7 +365,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
           const KickDesc K = is_pre ? A.pre : A.post;
           const int site = k < c ? k : s + k - c;
           double2 m[4];
-          if ((act & (1 << k)) && site < A.L_real) {
+          if ((act & ~(int)K.skip & (1 << k)) && site < A.L_real) {
             build_site_kick(A, K, site, traj, m);
           } else {  // inactive tile bits and padding sites: identity
             m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);

@@ -188,6 +188,29 @@ class DtcEngine:
             ctypes.c_int32(int(inverse)), _capi.as_dptr(buf), _capi.as_dptr(z)))
         return psi, z
 
+    # -- sharded state (dtc_shard_*; driver: sharded.py) ----------------
+    def shard_set_basis(self, spec: SweepSpec, shard, state_ptr: int, seed: int = 0x5EED0001,
+                        traj: int = 0):
+        """Prepare the (noisy-prep) product state in device buffer ``state_ptr``."""
+        _capi.check(self._lib.dtc_shard_set_basis(
+            self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
+            ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
+            ctypes.c_void_p(state_ptr)))
+
+    def shard_step(self, spec: SweepSpec, shard, period: int, pre_mask: int, diag: bool,
+                   post_mask: int, src_ptr: int, dst_ptr: int, want_obs: bool = False,
+                   seed: int = 0x5EED0001, traj: int = 0, inst: int = 0):
+        """dst = K_{period+1}[post] . D^diag . K_period[pre] . src on every shard held;
+        returns obs [n_shards][1 + n_local] (or None)."""
+        obs = np.zeros((shard.n_shards, 1 + shard.n_local)) if want_obs else None
+        _capi.check(self._lib.dtc_shard_step(
+            self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
+            ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
+            ctypes.c_int32(inst), ctypes.c_int32(period), ctypes.c_uint64(pre_mask),
+            ctypes.c_int32(int(bool(diag))), ctypes.c_uint64(post_mask),
+            ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr), _capi.as_dptr(obs)))
+        return obs
+
     # -- profiling -------------------------------------------------------
     def set_profiling(self, on: bool):
         _capi.check(self._lib.dtc_set_profiling(self._ctx, int(on)))

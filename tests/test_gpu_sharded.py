@@ -1,0 +1,58 @@
+"""The sharded single-state engine path (dtc_shard_*, sharded.py; config C5)
+on one GPU with virtual ranks (all 2^k shards in one process, exchange = a
+strided device copy) against the single-device engine (dtc_autocorr) on the
+same trajectory: per-site <Z_i(t)> to 1e-10 — the engine's effective-field
+diagonal tables, the bit-map-aware kicks and noise (RNG keyed by logical site)
+and the Z bookkeeping of rank bits.  The L=34 / 8-rank run itself is the same
+code with collective_exchange over RCCL (bench.py --config c5)."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from tests.helpers import random_disorder
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def stepper(pkg, engine):
+    return pkg.sharded.EngineStepper(engine)
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (14, 1, 6, 0.0, "vacuum", "x", 0),
+    (14, 2, 6, 0.1, "neel", "circular_left", 0),
+    (15, 3, 5, 0.05, "neel", "xy", 1),
+    (18, 2, 6, 0.05, "vacuum", "y", 0),
+    (22, 3, 5, 0.05, "neel", "x", 0),
+    (26, 3, 4, 0.0, "vacuum", "x", 0),
+])
+def test_virtual_shards_match_engine(pkg, engine, stepper, L, k, T, p, state, pol, toff):
+    rng = np.random.default_rng(L * 7 + k)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    one = dataclasses.replace(spec, hs=hs[1:2], phis=phis[1:2])
+    for traj in (0, 5):
+        got = pkg.sharded.sharded_forward(stepper, spec, k, inst=1, traj=traj, seed=77)
+        ref = engine.autocorr(one, 1, seed=77, traj_offset=traj, want_echo=False,
+                              want_zsite=True)
+        assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+        assert np.abs(got["fwd"] - ref["fwd"][0, 0]).max() < TOL
+        assert np.abs(got["norm"] - 1.0).max() < 1e-10
+
+
+def test_l30_eight_virtual_ranks(pkg, engine, stepper):
+    """C5's layout (3 rank bits) at the largest size that also fits whole."""
+    import os
+
+    L = 30
+    hs, phis = pkg.load_disorder(34, 1, os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "data"))
+    spec = pkg.SweepSpec(L=L, T=4, hs=hs, phis=phis, g=0.97, use_noise=0)
+    got = pkg.sharded.sharded_forward(stepper, spec, 3)
+    ref = engine.autocorr(spec, 1, want_echo=False, want_zsite=True)
+    assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+    assert np.abs(got["zsite"][1] - np.cos(np.pi * 0.97)).max() < 1e-12

@@ -1,0 +1,124 @@
+"""The sharded single-state path (sharded.py, config C5) on CPU: the sweep
+driver with the numpy step (oracle/shard_oracle.py) in place of the engine,
+virtual ranks in one process and real ranks over gloo (all_to_all_single),
+against the whole-state C oracle per trajectory.  The engine's own step is
+checked against dtc_autocorr on the GPU (tests/test_gpu_sharded.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import c_oracle
+from oracle.shard_oracle import NumpyShardStepper
+from tests.helpers import random_disorder
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _spec(pkg, L, T, p=0.1, state="neel", pol="circular_left", toff=0, seed=4):
+    rng = np.random.default_rng(seed)
+    hs, phis = random_disorder(rng, L, 2)
+    return pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.91, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+
+
+def _halves(n):
+    """Two site groups (as the engine has for 13 <= n <= 21): the post-kick of a
+    period then covers only the top group and the next period's first step
+    kicks the rest."""
+    lo = (1 << (n // 2)) - 1
+    return [lo, ((1 << n) - 1) ^ lo]
+
+
+def test_plan_groups_partition(pkg):
+    for n in (12, 13, 20, 21, 22, 28, 31, 32):
+        gs = pkg._capi.plan_groups(n)
+        acc = 0
+        for g in gs:
+            assert acc & g == 0
+            acc |= g
+        assert acc == (1 << n) - 1
+    assert len(pkg._capi.plan_groups(20)) == 2
+    assert len(pkg._capi.plan_groups(31)) == 4
+
+
+def test_layout_exchange_roundtrip(pkg):
+    sh = pkg.sharded
+    lay = sh.initial_layout(10, 2)
+    y = lay.exchanged()
+    assert y.site_of[6:8] == (8, 9) and y.site_of[8:10] == (6, 7)
+    assert y.exchanged() == lay
+    with pytest.raises(ValueError):
+        sh.initial_layout(5, 2)
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (6, 1, 6, 0.0, "vacuum", "x", 0),
+    (7, 2, 6, 0.1, "neel", "circular_left", 0),
+    (9, 3, 5, 0.05, "neel", "xy", 1),
+])
+@pytest.mark.parametrize("groups", [None, _halves])
+def test_virtual_ranks_match_oracle(pkg, L, k, T, p, state, pol, toff, groups):
+    spec = _spec(pkg, L, T, p, state, pol, toff)
+    for traj in (0, 3):
+        got = pkg.sharded.sharded_forward(NumpyShardStepper(groups), spec, k, inst=1,
+                                          traj=traj, seed=99)
+        # the whole-state oracle for instance 1, trajectory traj
+        import dataclasses
+        one = dataclasses.replace(spec, hs=spec.hs[1:2], phis=spec.phis[1:2])
+        ref = c_oracle.autocorr(one, 1, seed=99, traj_offset=traj, want_zsite=True,
+                                want_echo=False)
+        assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < 1e-12
+        assert np.abs(got["fwd"] - ref["fwd"][0, 0]).max() < 1e-12
+        assert np.abs(got["norm"] - 1.0).max() < 1e-12
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, k, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from __graft_entry__ import load_package
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = load_package()
+    spec = _spec(pkg, 8, 5)
+    out = pkg.sharded.sharded_forward(NumpyShardStepper(_halves), spec, k, inst=0, traj=2,
+                                      seed=5, rank=rank, world=world)
+    if rank == 0:
+        q.put(out["zsite"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_gloo_ranks_match_oracle(pkg, k):
+    world = 1 << k
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=180)
+    for pr in procs:
+        pr.join(timeout=180)
+        assert pr.exitcode == 0
+    import dataclasses
+    spec = _spec(pkg, 8, 5)
+    one = dataclasses.replace(spec, hs=spec.hs[:1], phis=spec.phis[:1])
+    ref = c_oracle.autocorr(one, 1, seed=5, traj_offset=2, want_zsite=True, want_echo=False)
+    assert np.abs(got - ref["zsite"][0, 0]).max() < 1e-12
