@@ -110,13 +110,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-traj", type=int, default=0, help="0 = one per host thread")
     ap.add_argument("--cpu-tf", type=int, default=8)
-    ap.add_argument("--config", choices=("c2", "c4"), default="c2",
+    ap.add_argument("--config", choices=("c2", "c4", "c5"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c4: L=28 "
-                         "noiseless disorder sweep, instances sharded over ranks")
+                         "noiseless disorder sweep, instances sharded over ranks; c5: one "
+                         "L=34 state sharded over the ranks (1 GPU: --L 31, 8 virtual ranks)")
+    ap.add_argument("--shard-bits", type=int, default=3, help="c5: log2 of the shard count")
     ap.add_argument("--instances", type=int, default=32, help="c4: instances per step per GPU")
     args = ap.parse_args()
     if args.config == "c4":
         return main_c4(args)
+    if args.config == "c5":
+        return main_c5(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -322,12 +326,12 @@ def main_c4(args):
         return
     per_inst = T - 1
     value = world * args.steps * n * per_inst / elapsed
-    state_bytes = 32.0 * (1 << L)
     lo_s, hi_s = stats[0], stats[1]
-    B = n  # one launch covers the step's batch (auto batch holds all n states)
     avg_lo = lo_s["total_ms"] / max(1, lo_s["launches"]) / 1e3
     avg_hi = hi_s["total_ms"] / max(1, hi_s["launches"]) / 1e3
-    launch_bytes = state_bytes * B
+    # algorithmic bytes per launch as the engine recorded them (32 B x 2^L x batch)
+    launch_bytes = lo_s["bytes"] / max(1, lo_s["launches"])
+    hi_bytes = hi_s["bytes"] / max(1, hi_s["launches"])
     achieved = launch_bytes / avg_lo / 1e9 if lo_s["launches"] else 0.0
     res = {
         "metric": "Floquet-periods×instances/sec at L=28 (C4); RZZ-kernel HBM GB/s vs peak",
@@ -346,10 +350,111 @@ def main_c4(args):
                      "avg_launch_ms": avg_lo * 1e3, "launches": lo_s["launches"]},
         "kernels": {"kdk_pass": {"launches": lo_s["launches"], "avg_ms": avg_lo * 1e3},
                     "kick_pass": {"launches": hi_s["launches"], "avg_ms": avg_hi * 1e3,
-                                  "GBps": launch_bytes / avg_hi / 1e9 if hi_s["launches"] else None},
+                                  "GBps": hi_bytes / avg_hi / 1e9 if hi_s["launches"] else None},
                     "kernel_time_frac": (lo_s["total_ms"] + hi_s["total_ms"] + stats[2]["total_ms"])
                     / (elapsed * 1e3)},
         "z_mean_t1": float(acc[1].mean().item() / (world * args.steps * n)),
+        "device": eng.device_info()["name"],
+    }
+    print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def main_c5(args):
+    """one noiseless state, L=34, tf=30, sharded over 8 ranks
+    (32 GiB per GPU), one all-to-all exchange per period (sharded.py).  On one
+    GPU the same driver runs 2^shard_bits virtual ranks (default L=31 there)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    torch.cuda.set_device(local_rank if world > 1 else 0)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+    pkg = importlib.import_module(PKG)
+    k = args.shard_bits
+    if world > 1 and world != (1 << k):
+        raise SystemExit("c5: world size must be 2^shard_bits")
+    L = args.L if args.L != 20 else (34 if world > 1 else 31)
+    T = args.tf
+    hs, phis = pkg.load_disorder(34, 1, os.path.join(ROOT, "data"))
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.97, use_noise=0)
+    eng = pkg.DtcEngine(local_rank)
+    stepper = pkg.sharded.EngineStepper(eng)
+    lay = pkg.sharded.initial_layout(L, k, rank * ((1 << k) // world), (1 << k) // world)
+    bufs = stepper.alloc(lay)
+    xt = [0.0]
+    W = 1 << k
+
+    def exchange(src, dst):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if world == 1:
+            pkg.sharded.virtual_exchange(src, dst, W)
+        else:
+            pkg.sharded.collective_exchange(src, dst)
+        torch.cuda.synchronize()
+        xt[0] += time.perf_counter() - t0
+
+    def step():
+        return pkg.sharded.sharded_forward(stepper, spec, k, rank=rank, world=world,
+                                           exchange=exchange, buffers=bufs)
+
+    for _ in range(args.warmup):
+        step()
+    eng.reset_stats()
+    eng.set_profiling(True)
+    xt[0] = 0.0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    stats = eng.kernel_stats()
+    el = torch.tensor([elapsed, xt[0]], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed, xch = float(el[0].item()), float(el[1].item())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    P = T - 1
+    lo_s, hi_s = stats[0], stats[1]
+    by = lo_s["bytes"] + hi_s["bytes"]
+    ms = lo_s["total_ms"] + hi_s["total_ms"]
+    achieved = by / (ms / 1e3) / 1e9 if ms else 0.0
+    shard_bytes = 16.0 * (1 << (L - k)) * lay.n_shards
+    res = {
+        "metric": f"Floquet-periods/sec, one L={L} state sharded over {W} ranks (C5)",
+        "value": args.steps * P / elapsed, "unit": "periods/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (data/hs_L34.csv row 0, seeded generate_disorder)",
+        "config": {"workload": (f"C5: one noiseless L={L} state, tf={T}, g=0.97, per-site "
+                                f"<Z_i(t)> every period, {W} shards "
+                                f"({'virtual, 1 GPU' if world == 1 else 'one per GPU'})"),
+                   "L": L, "tf": T, "shards": W, "parallelism": f"state-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "all pass kernels (kick / K-D-K), per-rank shard",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+        "exchange": {"total_s": xch, "per_period_ms": xch / (args.steps * P) * 1e3,
+                     "bytes_per_period_per_rank": shard_bytes * (W - 1) / W,
+                     "kind": "strided device copy" if world == 1 else "RCCL all_to_all_single"},
+        "pass_time_frac": ms / 1e3 / elapsed,
+        "z_t1_mean": float(out["zsite"][1].mean()),
+        "kat_cos_pi_g": float(np.cos(np.pi * 0.97)),
         "device": eng.device_info()["name"],
     }
     print(json.dumps(res), flush=True)

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -709,6 +710,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   if (B <= 0) {
     size_t free_b = 0, total_b = 0;
     DTC_HIP(hipMemGetInfo(&free_b, &total_b));
+    free_b += ctx->F.n + ctx->E.n;  // the batch buffers this call may reuse or regrow
     // small states: ~64 GiB of batch saturates the device; large states
     // (L >= 24, C4-style instance batches) may use most of the 288 GB
     double budget = per_state >= (double)(256ull << 20)
@@ -720,6 +722,13 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   }
   B = std::min<int64_t>(B, S);
   B = std::min<int64_t>(B, 65535);
+  if (std::getenv("DTC_VERBOSE")) {
+    size_t fr = 0, to = 0;
+    (void)hipMemGetInfo(&fr, &to);
+    std::fprintf(stderr, "[dtc] L=%d states=%lld batch=%lld state=%.3f GiB free=%.1f/%.1f GiB\n",
+                 L, (long long)S, (long long)B, per_state / (1 << 30), fr / 1073741824.0,
+                 to / 1073741824.0);
+  }
 
   DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
   if (want_e) DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));

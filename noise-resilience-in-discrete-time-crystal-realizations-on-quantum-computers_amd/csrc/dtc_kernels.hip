@@ -425,6 +425,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
                                                  x0 | M.rel(r << (4 * LAY)))));
       }
     };
+    // Observables of the tile: (sum |a|^2, sum z_i |a|^2 for the probe or every
+    // site).  Only sites inside the tile need a reduction: a register bit of the
+    // layout from per-thread partial sums, a thread bit from the signed thread
+    // total; a site outside the tile has one sign over the tile (tbase).
     auto measure_in = [&](auto lay_tag) {
       constexpr int LAY = decltype(lay_tag)::value;
       const int64_t x0 = M.at(ybase<LAY>(t));
@@ -436,25 +440,42 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
         ptot += pr[r];
       }
+      double zr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double z = 0.0;
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
+        zr[j] = z;
+      }
       double tot = wave_sum(ptot);
       if (PERSIST) __syncthreads();  // s_red of the previous tile consumed
       if (lane == 0) s_red[wave][0] = tot;
-      const int n_z = A.meas == kMeasProbe ? 1 : A.L_real;
+      const bool probe_only = A.meas == kMeasProbe;
+      const int n_z = probe_only ? 1 : A.L_real;
+      auto tile_bit = [&](int site) {
+        return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+      };
       for (int i = 0; i < n_z; ++i) {
-        const int site = A.meas == kMeasProbe ? A.probe : i;
-        double z = 0.0;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-          const int64_t x = x0 | M.rel(r << (4 * LAY));
-          z += ((x >> site) & 1) ? -pr[r] : pr[r];
-        }
+        const int site = probe_only ? A.probe : i;
+        const int tb = tile_bit(site);
+        if (tb < 0) continue;
+        const int j = tb - 4 * LAY;
+        double z;
+        if (j >= 0 && j < 4)
+          z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
+        else
+          z = ((x0 >> site) & 1) ? -ptot : ptot;
         z = wave_sum(z);
         if (lane == 0) s_red[wave][1 + i] = z;
       }
       __syncthreads();
       if (t < A.n_obs) {
+        const int site = probe_only ? A.probe : t - 1;
+        const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
         double acc = 0.0;
-        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
+        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
+        if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
         A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
       }
     };
@@ -581,21 +602,39 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
   }
 }
 
-__global__ void reduce_kernel(const double* __restrict__ partial, int n_tiles, int n_obs,
-                              int batch, double* __restrict__ out, int64_t out_stride) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= batch * n_obs) return;
-  const int b = i / n_obs, o = i - b * n_obs;
-  const double* p = partial + (int64_t)b * n_tiles * n_obs + o;
-  double acc = 0.0;
-  for (int k = 0; k < n_tiles; ++k) acc += p[(int64_t)k * n_obs];
-  out[(int64_t)b * out_stride + o] = acc;
+// out[b][o] = sum over tiles of partial[b][tile][o]: one workgroup per
+// (state, 8 observables), fixed summation order (strided per thread, then an
+// LDS tree), so results do not depend on the batch a state ran in.
+__global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partial,
+                                                     int n_tiles, int n_obs, int batch,
+                                                     double* __restrict__ out,
+                                                     int64_t out_stride) {
+  __shared__ double s_acc[8][256];
+  const int b = blockIdx.y, o0 = blockIdx.x * 8, t = threadIdx.x;
+  const int no = min(8, n_obs - o0);
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = t; k < n_tiles; k += 256) {
+    const double* p = partial + ((int64_t)b * n_tiles + k) * n_obs + o0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < no) acc[j] += p[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s_acc[j][t] = acc[j];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_acc[j][t] += s_acc[j][t + w];
+    }
+    __syncthreads();
+  }
+  if (t < no) out[(int64_t)b * out_stride + o0 + t] = s_acc[t][0];
 }
 
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
                          double* out, int64_t out_stride, hipStream_t stream) {
-  const int n = batch * n_obs;
-  hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, partial,
+  hipLaunchKernelGGL(reduce_kernel, dim3((n_obs + 7) / 8, batch), dim3(256), 0, stream, partial,
                      n_tiles, n_obs, batch, out, out_stride);
   return hipGetLastError();
 }
