@@ -165,6 +165,18 @@ int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise
  * (bit masks, one per group; returns the count or a negative error). */
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups);
 
+/* Energy observables of the forward sweep (the
+ * BackendEstimatorV2 runs of autocorr-delta-a-single-qiskit-fast-energy*.py:
+ * L-qubit circuit of fast.py's periods with no ancilla, energy.py:136-173).
+ * Per trajectory and t (same schedule, noise and RNG contract as dtc_autocorr):
+ *   z  [n_inst][n_traj][T][L]    <Z_i>
+ *   zz [n_inst][n_traj][T][L-1]  <Z_i Z_{i+1}>      (nullable when L = 1)
+ *   x  [n_inst][n_traj][T][L]    <X_i> (noiseless X-basis measurement)
+ * in little-endian site order; the caller forms any Hamiltonian from them
+ * (energy.py:83-102 builds its labels big-endian, see energy.py here). */
+int dtc_energy(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise, uint64_t seed,
+               int64_t traj_offset, int32_t n_traj, double* z, double* zz, double* x);
+
 /* Profiling: when enabled, every kernel launch is bracketed by HIP events on
  * the ctx stream and accumulated per kernel kind. */
 #define DTC_KERNEL_LO_PASS 0   /* fused RZZ+RZ diagonal + low-site kick pass */

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "dtc_shard_set_basis",
     "dtc_shard_step",
     "dtc_plan_groups",
+    "dtc_energy",
 )
 
 KERNEL_LO_PASS = 0
@@ -140,6 +141,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, _dp,
+        ]
+        lib.dtc_energy.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), ctypes.c_uint64, ctypes.c_int64,
+            ctypes.c_int32, _dp, _dp, _dp,
         ]
         lib.dtc_plan_groups.argtypes = [ctypes.c_int32, P(ctypes.c_uint64), ctypes.c_int32]
         for name in EXPORTED_SYMBOLS:

@@ -355,7 +355,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
   for (const KickDesc* k : {&ps.pre, &ps.post}) {
     if (!k->enabled) continue;
-    const int rk = rc.row_kind[k->row];
+    const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
+    const int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
     kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
   }
   const int kernel = has_d ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
@@ -884,6 +885,122 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
   return DTC_OK;
 }
 
+
+int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,
+               int64_t traj_offset, int32_t n_traj, double* z, double* zz, double* x) {
+  if (!ctx || !z || !x || (!zz && pr && pr->L > 1)) return fail(DTC_EINVAL, "null ctx/outputs");
+  DTC_TRY(check_problem(pr, nz));
+  if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
+  if (traj_offset < 0) return fail(DTC_EINVAL, "traj_offset must be >= 0");
+  DTC_HIP(hipSetDevice(ctx->device));
+
+  RunCfg rc;
+  rc.prob = pr;
+  rc.pl = make_plan(pr->L);
+  rc.seed = seed;
+  rc.traj_offset = traj_offset;
+  rc.n_traj = n_traj;
+  rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
+  thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  const Plan& pl = rc.pl;
+  const int T = pr->T, L = pr->L;
+  const int P = T - 1 + pr->t_offset;
+  const int n_e = 2 * L;   // norm, Z_i, Z_i Z_i+1
+  const int n_x = 1 + L;   // norm, X_i (Z after H)
+  DTC_TRY(upload_tables(ctx, pr, pl));
+
+  const int64_t S = (int64_t)pr->n_inst * n_traj;
+  const double per_state = (double)pl.len * 32.0;
+  int64_t B = pr->batch;
+  if (B <= 0) {
+    size_t free_b = 0, total_b = 0;
+    DTC_HIP(hipMemGetInfo(&free_b, &total_b));
+    free_b += ctx->F.n + ctx->E.n;
+    const double budget = std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
+    B = std::max<int64_t>(1, std::min<int64_t>((int64_t)(budget / per_state), 4096));
+  }
+  B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
+  DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
+  DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));
+  DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * std::max(n_e, n_x) * sizeof(double)));
+  DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_e * sizeof(double)));
+  DTC_TRY(ensure(ctx->vals_e, (size_t)B * T * n_x * sizeof(double)));
+  DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
+  std::vector<double> hv_f((size_t)B * T * n_e), hv_x((size_t)B * T * n_x);
+  std::vector<int64_t> masks(B);
+
+  for (int64_t bs = 0; bs < S; bs += B) {
+    const int nb = (int)std::min<int64_t>(B, S - bs);
+    for (int b = 0; b < nb; ++b)
+      masks[b] = (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + (bs + b) % n_traj));
+    double2* F = (double2*)ctx->F.p;
+    double2* E = (double2*)ctx->E.p;
+    DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
+                           hipMemcpyHostToDevice, ctx->stream));
+    DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
+    DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+    DTC_HIP(hipMemsetAsync(ctx->vals_f.p, 0, (size_t)nb * T * n_e * sizeof(double), ctx->stream));
+    DTC_HIP(hipMemsetAsync(ctx->vals_e.p, 0, (size_t)nb * T * n_x * sizeof(double), ctx->stream));
+    if (P > 0) {
+      Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
+      while (!fw.done()) {
+        PassSpec ps = next_pass(fw);
+        const int p = ps.d_index;
+        const int t = p - pr->t_offset;
+        const bool closes = ps.diag != dtc::kDiagNone;
+        const bool meas = closes && t >= 0;
+        DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, ps, F, F,
+                                 meas ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_e,
+                                 meas ? (double*)ctx->vals_f.p + (size_t)t * n_e : nullptr,
+                                 (int64_t)T * n_e));
+        if (!meas) continue;
+        // X basis: E = H^L . (undo of the kick a group is already ahead by) . F
+        const int G = (int)pl.groups.size();
+        for (int g = 0; g < G; ++g) {
+          PassSpec xs{g, no_kick(), no_kick(), dtc::kDiagNone, 0};
+          xs.pre = fw.kc[g] > p
+                       ? dtc::KickDesc{1, p, dtc::kKickUndoBasisX, dtc::kStreamForward,
+                                       (uint32_t)(p + 1)}
+                       : dtc::KickDesc{1, 0, dtc::kKickBasisX, 0u, 0u};
+          const bool last = g == G - 1;
+          DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, xs, g == 0 ? F : E, E,
+                                   last ? dtc::kMeasSites : dtc::kMeasNone, 1, n_x,
+                                   last ? (double*)ctx->vals_e.p + (size_t)t * n_x : nullptr,
+                                   (int64_t)T * n_x));
+        }
+      }
+    }
+    DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_e * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    DTC_HIP(hipMemcpyAsync(hv_x.data(), ctx->vals_e.p, (size_t)nb * T * n_x * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    DTC_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->prof) DTC_TRY(resolve_pending(ctx));
+    for (int b = 0; b < nb; ++b) {
+      const int64_t g = bs + b;
+      const uint64_t m = (uint64_t)masks[b];
+      for (int t = 0; t < T; ++t) {
+        const bool at_init = (t + pr->t_offset == 0);
+        const double* vf = hv_f.data() + ((size_t)b * T + t) * n_e;
+        const double* vx = hv_x.data() + ((size_t)b * T + t) * n_x;
+        double* zo = z + ((size_t)g * T + t) * L;
+        double* xo = x + ((size_t)g * T + t) * L;
+        for (int i = 0; i < L; ++i) {
+          zo[i] = at_init ? (((m >> i) & 1ull) ? -1.0 : 1.0) : vf[1 + i];
+          xo[i] = at_init ? 0.0 : vx[1 + i];
+        }
+        if (L > 1) {
+          double* zzo = zz + ((size_t)g * T + t) * (L - 1);
+          for (int i = 0; i + 1 < L; ++i)
+            zzo[i] = at_init ? ((((m >> i) ^ (m >> (i + 1))) & 1ull) ? -1.0 : 1.0)
+                             : vf[1 + L + i];
+        }
+      }
+    }
+  }
+  return DTC_OK;
+}
 
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups) {
   if (n_bits < 1 || n_bits > 40 || !masks) return fail(DTC_EINVAL, "bad arguments");

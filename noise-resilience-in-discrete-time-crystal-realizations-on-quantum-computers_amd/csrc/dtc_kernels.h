@@ -14,10 +14,15 @@ static constexpr int kThreads = 256;
 static constexpr int kRegs = 16;          // amplitudes per thread (4 register bits)
 static constexpr int kChunkBits = 5;      // diagonal factor tables: 5 sites + next bit
 static constexpr int kMaxChunks = 8;      // L_eff <= 40
-static constexpr int kMaxObs = 1 + 40;    // norm + per-site <Z_i>
+static constexpr int kMaxObs = 64;        // norm + per-site <Z_i> + per-bond <Z_i Z_i+1> (L <= 32)
 
 enum DiagMode { kDiagNone = 0, kDiagFwd = 1, kDiagConj = 2 };
-enum MeasMode { kMeasNone = 0, kMeasProbe = 1, kMeasSites = 2 };
+enum MeasMode {
+  kMeasNone = 0,
+  kMeasProbe = 1,   // (norm, Z_probe)
+  kMeasSites = 2,   // (norm, Z_0 .. Z_{L-1})
+  kMeasEnergy = 3,  // (norm, Z_0 .. Z_{L-1}, Z_0 Z_1 .. Z_{L-2} Z_{L-1})
+};
 // Which parts a pass runs: pre-kick (K), diagonal (D), post-kick (K).
 enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4 };
 // Matrix family of every kick in a pass (chosen by the host from the kick
@@ -30,6 +35,8 @@ enum KickMode {
   kKickForward = 0,  // M = P_n G_n ... P_1 G_1            (forward period, noisy)
   kKickInverse = 1,  // M = P_n G_1^+ ... P_1 G_n^+        (UF.inverse(), noisy)
   kKickUndo = 2,     // M = (forward M)^+                  (exact undo, same draws)
+  kKickBasisX = 3,   // M = H                              (X-basis measurement, noiseless)
+  kKickUndoBasisX = 4,  // M = H (forward M)^+             (undo a pending kick, then H)
 };
 
 struct KickDesc {
@@ -83,7 +90,7 @@ struct PassArgs {
   int meas;                // MeasMode
   int probe;
   int meas_at_end;         // measure after the post-kick instead of after the diagonal
-  int n_obs;               // kMeasProbe: 2 (norm, Z_probe); kMeasSites: 1 + L_real
+  int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 2 L_real
   double* partial;         // [B][n_tiles][n_obs]
 };
 

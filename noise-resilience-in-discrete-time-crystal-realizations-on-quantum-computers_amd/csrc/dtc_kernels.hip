@@ -118,6 +118,12 @@ __device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, 
   m[3] = make_double2(1.0, 0.0);
   const bool inv = (K.mode == kKickInverse);
   if (A.site_of) site = A.site_of[site];  // sharded state: physical bit -> logical site
+  if (K.mode == kKickBasisX) {
+    const double r = 0.70710678118654752440;
+    m[0] = make_double2(r, 0.0); m[1] = make_double2(r, 0.0);
+    m[2] = make_double2(r, 0.0); m[3] = make_double2(-r, 0.0);
+    return;
+  }
   for (int q = 0; q < A.n_sub; ++q) {
     const int qq = inv ? (A.n_sub - 1 - q) : q;
     const double2* gp = A.kick + (((int64_t)K.row * A.L_kick + site) * A.n_sub + qq) * 4;
@@ -130,7 +136,13 @@ __device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, 
       pauli_left(m, p);
     }
   }
-  if (K.mode == kKickUndo) dagger(m);
+  if (K.mode == kKickUndo || K.mode == kKickUndoBasisX) dagger(m);
+  if (K.mode == kKickUndoBasisX) {
+    const double r = 0.70710678118654752440;
+    double2 h[4] = {make_double2(r, 0.0), make_double2(r, 0.0), make_double2(r, 0.0),
+                    make_double2(-r, 0.0)};
+    mat_mul(m, h, m);
+  }
 }
 
 // Per-site kick of a pass, canonicalised for the pass's matrix family:
@@ -469,10 +481,24 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         z = wave_sum(z);
         if (lane == 0) s_red[wave][1 + i] = z;
       }
+      if (A.meas == kMeasEnergy) {
+        // bond correlators <Z_i Z_i+1>: sign per amplitude, generic reduction
+        for (int i = 0; i + 1 < A.L_real; ++i) {
+          double z = 0.0;
+#pragma unroll
+          for (int r = 0; r < kRegs; ++r) {
+            const int64_t x = x0 | M.rel(r << (4 * LAY));
+            z += (((x >> i) ^ (x >> (i + 1))) & 1) ? -pr[r] : pr[r];
+          }
+          z = wave_sum(z);
+          if (lane == 0) s_red[wave][1 + A.L_real + i] = z;
+        }
+      }
       __syncthreads();
       if (t < A.n_obs) {
         const int site = probe_only ? A.probe : t - 1;
-        const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
+        const bool is_site = t >= 1 && t <= n_z;
+        const int ws = (!is_site || tile_bit(site) >= 0) ? t : 0;
         double acc = 0.0;
         for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
         if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;

@@ -1,0 +1,171 @@
+"""Energy observable path: the
+``autocorr-delta-a-single-qiskit-fast-energy*.py`` family.
+
+The reference builds an L-qubit circuit (no ancilla; optional neel X gates,
+then t periods of fast.py's U_F; energy.py:136-150) and estimates
+``<H>`` with ``BackendEstimatorV2`` on AerSimulator under the same
+depolarizing model.  ``H`` comes from ``get_hamiltonian`` (energy.py:83-102):
+
+    labels built as strings: position i of "I"*L gets Z (coeff hs[i]),
+    positions i, i+1 get ZZ (coeff phis[i]), position i gets X (coeff g*pi).
+
+Qiskit Pauli labels are big-endian — string position i is qubit L-1-i — so
+the terms act as ``hs[i] Z_{L-1-i}``, ``phis[i] Z_{L-2-i} Z_{L-1-i}`` and
+``g pi X_{L-1-i}``: the fields are applied to the chain in reverse order
+relative to the circuit's RZ(hs[i]) on qubit i.  ``hamiltonian_coefficients``
+returns the little-endian per-site arrays that reproduce this exactly
+(checked against the literal label construction in tests/test_energy_cpu.py).
+
+Execution: one C-ABI call (``dtc_energy``) returns per-trajectory
+``<Z_i>(t)``, ``<Z_i Z_i+1>(t)`` and ``<X_i>(t)`` (X basis measured
+noiselessly, as Aer executes the estimator's appended basis change outside the
+noise model's u1/u2/u3 gates); any Hamiltonian variant of the scripts
+("full", "z_only", "zz_only", "x_only", "z_zz") is a linear combination.
+
+Noise accumulation (energy.py:212-218): the script adds
+``depolarizing_error(nprob)`` to ONE NoiseModel inside its loop over
+``nprobs``, so Aer composes the errors; depolarizing channels compose to
+``1 - prod(1 - p_k)``.  ``accumulated_noise`` mirrors that.
+
+Estimator: the reference's ``BackendEstimatorV2`` default precision 1/64
+means 4096 shots per measurement basis; here the trajectory mean (each
+trajectory an exact expectation) estimates the same quantity.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+
+from .engine import SweepSpec
+
+HAMILTONIAN_TYPES = ("full", "z_only", "zz_only", "x_only", "z_zz")
+ESTIMATOR_SHOTS = int(math.ceil(1.0 / 0.015625 ** 2))  # BackendEstimatorV2 default precision
+
+
+def hamiltonian_labels(L: int, g: float, hs, phis, hamiltonian_type: str = "full"):
+    """The reference's (label, coeff) list, big-endian labels (energy.py:83-102,
+    ham-comparison.py:85-115)."""
+    if hamiltonian_type not in HAMILTONIAN_TYPES:
+        raise ValueError(f"hamiltonian_type must be one of {HAMILTONIAN_TYPES}")
+    out = []
+    base = "I" * L
+    if hamiltonian_type in ("full", "z_only", "z_zz"):
+        for i in range(L):
+            out.append((base[:i] + "Z" + base[i + 1:], float(hs[i])))
+    if hamiltonian_type in ("full", "zz_only", "z_zz"):
+        for i in range(L - 1):
+            out.append((base[:i] + "ZZ" + base[i + 2:], float(phis[i])))
+    if hamiltonian_type in ("full", "x_only"):
+        for i in range(L):
+            out.append((base[:i] + "X" + base[i + 1:], float(g) * np.pi))
+    return out
+
+
+def hamiltonian_coefficients(L: int, g: float, hs, phis, hamiltonian_type: str = "full"):
+    """Little-endian per-site coefficients ``(cz[L], czz[L-1], cx[L])`` with
+    ``H = sum_q cz[q] Z_q + sum_q czz[q] Z_q Z_q+1 + sum_q cx[q] X_q``."""
+    cz = np.zeros(L)
+    czz = np.zeros(max(L - 1, 0))
+    cx = np.zeros(L)
+    for label, c in hamiltonian_labels(L, g, hs, phis, hamiltonian_type):
+        qubits = [L - 1 - i for i, ch in enumerate(label) if ch != "I"]
+        kind = label.replace("I", "")
+        if kind == "Z":
+            cz[qubits[0]] += c
+        elif kind == "ZZ":
+            czz[min(qubits)] += c
+        elif kind == "X":
+            cx[qubits[0]] += c
+        else:  # pragma: no cover - labels are built above
+            raise ValueError(label)
+    return cz, czz, cx
+
+
+def energy_from_observables(obs: dict, L: int, g: float, hs, phis,
+                            hamiltonian_type: str = "full") -> np.ndarray:
+    """<H> per (..., t) from per-site observables ``z``, ``zz``, ``x``."""
+    cz, czz, cx = hamiltonian_coefficients(L, g, hs, phis, hamiltonian_type)
+    e = obs["z"] @ cz + obs["x"] @ cx
+    if L > 1:
+        e = e + obs["zz"] @ czz
+    return e
+
+
+def accumulated_noise(nprobs) -> list:
+    """Effective depolarizing parameter of each pass of the reference's loop
+    that keeps adding errors to one NoiseModel (energy.py:212-218)."""
+    out, keep = [], 1.0
+    for p in nprobs:
+        keep *= 1.0 - float(p)
+        out.append(1.0 - keep)
+    return out
+
+
+def _engine(engine):
+    if engine is not None:
+        return engine
+    from . import sweep
+
+    return sweep._default_engine()
+
+
+def get_instances_energy(spec: SweepSpec, n_traj: int = ESTIMATOR_SHOTS,
+                         hamiltonian_types=("full",), seed: int = 0x5EED0001, engine=None,
+                         traj_offset: int = 0) -> dict:
+    """``get_instances`` of the energy scripts: ``<H>(t)`` per instance
+    (``[inst][T]``) for each requested Hamiltonian variant, as the trajectory
+    mean of the engine's per-trajectory observables."""
+    obs = _engine(engine).energy(spec, n_traj, seed=seed, traj_offset=traj_offset)
+    out = {}
+    for ht in hamiltonian_types:
+        per = np.stack([
+            energy_from_observables({k: v[i] for k, v in obs.items()}, spec.L, _g0(spec.g),
+                                    spec.hs[i], spec.phis[i], ht)
+            for i in range(spec.n_inst)])
+        out[ht] = per.mean(axis=1)
+    return out
+
+
+def _g0(g):
+    return float(g[0]) if isinstance(g, (list, tuple, np.ndarray)) else float(g)
+
+
+# ---- the scripts' drivers and output files ---------------------------------------
+
+def energy_folder(L: int, variant: str = "full-ham") -> str:
+    """energy.py:59 (``full-ham``), ham-comparison.py:59 (``ham-comparison``),
+    energy-fakebrisbane.py:58 (``fakebrisbane``)."""
+    return f"energy-data_L{L}-{variant}"
+
+
+def energy_csv_name(prefix, state, g, L, inst, randomphi, delta, amplitude, noise, use_noise):
+    return (f"{prefix}_{state}_g{g}_L{L}_inst{inst}_randomphi{randomphi}_delta{delta}"
+            f"_amplitude{amplitude}_noise{noise}_usenoise{use_noise}.csv")
+
+
+def run_energy(L, g, hs, phis, T, nprobs=(0, 0.001, 0.01, 0.1), use_noise=1,
+               initial_state="vacuum", n_traj=ESTIMATOR_SHOTS, seed=0x5EED0001,
+               hamiltonian_types=("full",), accumulate=True, engine=None):
+    """energy.py's main loop (:212-222): for each nprob, ``av_energy / L`` per
+    Hamiltonian variant.  Returns ``{(ht, nprob): [T]}``."""
+    eff = accumulated_noise(nprobs) if accumulate else [float(p) for p in nprobs]
+    res = {}
+    for nprob, p_eff in zip(nprobs, eff):
+        spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
+                         noise_prob=p_eff, use_noise=use_noise)
+        per = get_instances_energy(spec, n_traj, hamiltonian_types, seed, engine)
+        for ht, v in per.items():
+            res[(ht, nprob)] = v.mean(axis=0) / L
+    return res
+
+
+def write_energy_csv(path: str, ts, columns: dict) -> str:
+    import pandas as pd
+
+    data = {"time": ts}
+    data.update(columns)
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    pd.DataFrame(data).to_csv(path, index=False)
+    return path

@@ -1,0 +1,97 @@
+"""Command line mirroring the energy scripts:
+
+    --mode full            autocorr-delta-a-single-qiskit-fast-energy.py (and -energy-envelope)
+                           nprobs = [0, 0.001, 0.01, 0.1], accumulated in one noise model
+                           (energy.py:209-222); columns energy_p_{nprob}
+    --mode ham-comparison  ...-energy-ham-comparison.py: nprobs = [noise_prob];
+                           columns energy_{z_only,zz_only,x_only,sum,full}_p_{nprob}
+    --mode vs-echo         ...-energy-ham-comparison-vs-echo.py: nprobs = [0.1];
+                           columns energy_{with,without}_x_p_{nprob}
+
+Flags as energy.py:26-40; files and folders as the scripts write them
+(energy.py:57-61, 229-234; ham-comparison.py:277-280; vs-echo.py:248-251).
+Values are ``mean over instances of <H>(t) / L``.  ``--use_fakebackend 1``
+needs FakeBrisbane calibration data, which is not available offline: error.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import numpy as np
+
+from . import energy as en
+from .disorder import load_disorder
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="DTC energy sweep on MI355X (HIP engine)")
+    p.add_argument("--mode", choices=("full", "ham-comparison", "vs-echo"), default="full")
+    p.add_argument("--L", type=int, default=4)
+    p.add_argument("--device_name", type=int, default=0)
+    p.add_argument("--inst", type=int, default=1)
+    p.add_argument("--randomphi", type=int, default=1)
+    p.add_argument("--phi_delta", type=float, default=0.0)
+    p.add_argument("--phi_amplitude", type=float, default=1.0)
+    p.add_argument("--tf", type=int, default=20)
+    p.add_argument("--g", type=float, default=0.97)
+    p.add_argument("--noise_prob", type=float, default=0.05)
+    p.add_argument("--use_noise", type=int, default=1)
+    p.add_argument("--initial_state", type=str, default="vacuum", choices=["vacuum", "neel"])
+    p.add_argument("--use_fakebackend", type=int, default=0)
+    p.add_argument("--trajectories", type=int, default=en.ESTIMATOR_SHOTS,
+                   help="trajectories per point (default: the estimator's 4096 shots)")
+    p.add_argument("--seed", type=int, default=0x5EED0001)
+    p.add_argument("--disorder_folder", type=str, default=".")
+    p.add_argument("--out_dir", type=str, default=".")
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    if args.use_fakebackend:
+        raise SystemExit("use_fakebackend=1: FakeBrisbane calibration data is not available "
+                         "offline (qiskit-ibm-runtime); see DESIGN.md")
+    L, T = args.L, args.tf
+    hs, phis = load_disorder(L, args.inst, args.disorder_folder)
+    ts = np.arange(0, T)
+    name_args = (args.initial_state, args.g, L, args.inst, args.randomphi, args.phi_delta,
+                 args.phi_amplitude, args.noise_prob, args.use_noise)
+    if args.mode == "full":
+        nprobs = [0, 0.001, 0.01, 0.1]
+        noisy = bool(args.use_noise)
+        res = en.run_energy(L, args.g, hs, phis, T, nprobs, use_noise=int(noisy),
+                            initial_state=args.initial_state, n_traj=args.trajectories,
+                            seed=args.seed)
+        cols = {f"energy_p_{p}": res[("full", p)] for p in nprobs}
+        path = os.path.join(args.out_dir, en.energy_folder(L, "full-ham"),
+                            en.energy_csv_name("energy_data", *name_args))
+    elif args.mode == "ham-comparison":
+        nprobs = [args.noise_prob]
+        res = en.run_energy(L, args.g, hs, phis, T, nprobs, use_noise=1,
+                            initial_state=args.initial_state, n_traj=args.trajectories,
+                            seed=args.seed,
+                            hamiltonian_types=("z_only", "zz_only", "x_only", "full"))
+        cols = {}
+        for p in nprobs:
+            cols[f"energy_z_only_p_{p}"] = res[("z_only", p)]
+            cols[f"energy_zz_only_p_{p}"] = res[("zz_only", p)]
+            cols[f"energy_x_only_p_{p}"] = res[("x_only", p)]
+            cols[f"energy_sum_p_{p}"] = res[("z_only", p)] + res[("zz_only", p)]
+            cols[f"energy_full_p_{p}"] = res[("full", p)]
+        path = os.path.join(args.out_dir, en.energy_folder(L, "ham-comparison"),
+                            en.energy_csv_name("energy_comparison_all", *name_args))
+    else:
+        nprobs = [0.1]
+        res = en.run_energy(L, args.g, hs, phis, T, nprobs, use_noise=1,
+                            initial_state=args.initial_state, n_traj=args.trajectories,
+                            seed=args.seed, hamiltonian_types=("full", "z_zz"))
+        cols = {}
+        for p in nprobs:
+            cols[f"energy_with_x_p_{p}"] = res[("full", p)]
+            cols[f"energy_without_x_p_{p}"] = res[("z_zz", p)]
+        path = os.path.join(args.out_dir, en.energy_folder(L, "ham-comparison"),
+                            en.energy_csv_name("energy_comparison", *name_args))
+    en.write_energy_csv(path, ts, cols)
+    print(f"Energy data saved to {path}")
+    return 0

@@ -188,6 +188,21 @@ class DtcEngine:
             ctypes.c_int32(int(inverse)), _capi.as_dptr(buf), _capi.as_dptr(z)))
         return psi, z
 
+    def energy(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
+               traj_offset: int = 0, batch: int = 0):
+        """Per-trajectory energy observables of the forward sweep (dtc_energy):
+        ``z`` [n_inst][n_traj][T][L], ``zz`` [..][L-1], ``x`` [..][L]."""
+        n_inst, T, L = spec.n_inst, spec.T, spec.L
+        z = np.zeros((n_inst, n_traj, T, L))
+        zz = np.zeros((n_inst, n_traj, T, max(L - 1, 0)))
+        x = np.zeros((n_inst, n_traj, T, L))
+        pr = self._problem(spec, True, False, batch, 0)
+        _capi.check(self._lib.dtc_energy(
+            self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)), ctypes.c_uint64(seed),
+            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(z),
+            _capi.as_dptr(zz) if L > 1 else None, _capi.as_dptr(x)))
+        return {"z": z, "zz": zz, "x": x}
+
     # -- sharded state (dtc_shard_*; driver: sharded.py) ----------------
     def shard_set_basis(self, spec: SweepSpec, shard, state_ptr: int, seed: int = 0x5EED0001,
                         traj: int = 0):

@@ -250,3 +250,39 @@ def statevector_zsite(L, T, hs, phis, kick, init_mask=0, t_offset=0):
             pr = np.abs(psi) ** 2
             out[t] = z @ pr
     return out
+
+
+def energy_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", t_offset=0):
+    """Exact <Z_i>, <Z_i Z_i+1>, <X_i> of the L-qubit energy circuit
+    (autocorr-delta-a-single-qiskit-fast-energy.py:136-150: optional neel X
+    gates, then t periods of fast.py's U_F, no ancilla) under the depolarizing
+    channel after every kick gate and prep X, for t = 0..T-1."""
+    N = 1 << L
+    x = np.arange(N)
+    w = np.ones(N)
+    for i in range(L):
+        flipped = initial_state == "neel" and (i + 1) % 2 == 0
+        pf = (1 - p / 2) if flipped else 0.0
+        b = (x >> i) & 1
+        w = w * np.where(b == 1, pf, 1 - pf)
+    rho = DM(L, np.diag(w).astype(np.complex128))
+    z = np.zeros((T, L))
+    zz = np.zeros((T, max(L - 1, 0)))
+    xs = np.zeros((T, L))
+    zbits = 1 - 2 * ((x[None, :] >> np.arange(L)[:, None]) & 1)
+    for s in range(T - 1 + t_offset + 1):
+        if s > 0:
+            _period(rho, 0, L, kick_gates_from_table(kick[s - 1]), hs, phis, p)
+        t = s - t_offset
+        if t < 0:
+            continue
+        m = rho.matrix()
+        d = np.real(np.diag(m))
+        z[t] = zbits @ d
+        for i in range(L - 1):
+            zz[t, i] = (zbits[i] * zbits[i + 1]) @ d
+        for i in range(L):
+            # <X_i> = 2 Re sum_{x: bit i = 0} rho[x ^ e_i, x]
+            lo = x[((x >> i) & 1) == 0]
+            xs[t, i] = 2.0 * np.real(m[lo ^ (1 << i), lo]).sum()
+    return z, zz, xs

@@ -1,0 +1,77 @@
+"""dtc_energy (HIP) vs the per-trajectory oracle (oracle/energy_oracle.py: the C
+oracle's periods + numpy observables): <Z_i>, <Z_i Z_i+1>, <X_i> per
+trajectory to 1e-10; the trajectory mean vs the exact density matrix."""
+import numpy as np
+import pytest
+
+from oracle import dm_oracle, energy_oracle
+from tests.helpers import random_disorder
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.mark.parametrize("L,T,p,state,pol", [
+    (4, 8, 0.05, "neel", "x"),
+    (7, 6, 0.1, "vacuum", "circular_left"),
+    (12, 5, 0.05, "neel", "xy"),
+    (14, 5, 0.05, "vacuum", "x"),
+    (17, 4, 0.02, "neel", "y"),
+])
+def test_energy_matches_oracle(pkg, engine, L, T, p, state, pol):
+    rng = np.random.default_rng(L + 100)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.94, noise_prob=p, polarization=pol,
+                         initial_state=state)
+    got = engine.energy(spec, 3, seed=21)
+    for inst in range(2):
+        for tr in range(3):
+            z, zz, x = energy_oracle.trajectory_energy(spec, inst, tr, seed=21)
+            assert np.abs(got["z"][inst, tr] - z).max() < TOL
+            assert np.abs(got["zz"][inst, tr] - zz).max() < TOL
+            assert np.abs(got["x"][inst, tr] - x).max() < TOL
+
+
+def test_energy_mean_vs_density_matrix(pkg, engine):
+    rng = np.random.default_rng(8)
+    L, T, p, n = 4, 10, 0.1, 4096
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.97, noise_prob=p)
+    got = engine.energy(spec, n, seed=3)
+    exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, p)
+    for k, key in enumerate(("z", "zz", "x")):
+        v = got[key][0]
+        mean, sd = v.mean(axis=0), v.std(axis=0) / np.sqrt(n) + 1e-12
+        assert np.all(np.abs(mean - exact[k]) < 5 * sd), key
+    e = pkg.energy.get_instances_energy(spec, 256, engine=engine)["full"]
+    assert e.shape == (1, T)
+
+
+@pytest.mark.parametrize("mode,cols", [
+    ("full", ["time", "energy_p_0", "energy_p_0.001", "energy_p_0.01", "energy_p_0.1"]),
+    ("ham-comparison", ["time", "energy_z_only_p_0.05", "energy_zz_only_p_0.05",
+                        "energy_x_only_p_0.05", "energy_sum_p_0.05", "energy_full_p_0.05"]),
+    ("vs-echo", ["time", "energy_with_x_p_0.1", "energy_without_x_p_0.1"]),
+])
+def test_energy_cli_files(pkg, golden, tmp_path, mode, cols):
+    import os
+
+    import pandas as pd
+
+    d = golden["disorder"]["L4"]
+    dis = tmp_path / "dis"
+    dis.mkdir()
+    pd.DataFrame(d["hs"]).to_csv(dis / "hs_L4.csv", index=False)
+    pd.DataFrame(d["phis"]).to_csv(dis / "phis_L4.csv", index=False)
+    out = tmp_path / "out"
+    rc = pkg.energy_cli.main(["--mode", mode, "--L", "4", "--tf", "6", "--trajectories", "128",
+                              "--disorder_folder", str(dis), "--out_dir", str(out)])
+    assert rc == 0
+    files = [os.path.join(r, f) for r, _, fs in os.walk(out) for f in fs]
+    assert len(files) == 1
+    df = pd.read_csv(files[0])
+    assert list(df.columns) == cols and len(df) == 6
+    if mode == "full":
+        # t = 0: <H>/L of the vacuum = (sum h_i) / L  (X terms vanish)
+        hs, _ = pkg.load_disorder(4, 1, str(dis))
+        assert abs(df["energy_p_0"][0] - hs[0].sum() / 4) < 1e-12
