@@ -72,6 +72,6 @@ def test_energy_cli_files(pkg, golden, tmp_path, mode, cols):
     df = pd.read_csv(files[0])
     assert list(df.columns) == cols and len(df) == 6
     if mode == "full":
-        # t = 0: <H>/L of the vacuum = (sum h_i) / L  (X terms vanish)
-        hs, _ = pkg.load_disorder(4, 1, str(dis))
-        assert abs(df["energy_p_0"][0] - hs[0].sum() / 4) < 1e-12
+        # t = 0: <H>/L of the vacuum = (sum h_i + sum phi_i) / L  (X terms vanish)
+        hs, phis = pkg.load_disorder(4, 1, str(dis))
+        assert abs(df["energy_p_0"][0] - (hs[0].sum() + phis[0].sum()) / 4) < 1e-12
