@@ -18,7 +18,8 @@ from . import _capi  # noqa: E402
 from .kicks import kick_table, POLARIZATIONS, rx, ry  # noqa: E402
 from .disorder import load_disorder, generate_disorder, save_disorder_to_csv  # noqa: E402
 from .engine import DtcEngine, SweepSpec, init_mask, N_ANCILLA_NOISY_GATES  # noqa: E402
-from . import circuit, aer, sweep, distributed, sharded, energy, cli, energy_cli  # noqa: E402
+from . import circuit, aer, sweep, distributed, sharded, energy, envelopes, control  # noqa: E402
+from . import cli, energy_cli, control_cli  # noqa: E402
 from .circuit import QuantumCircuit, transpile_aer_basis  # noqa: E402
 from .aer import AerSimulator, DtcSimulator, NoiseModel, depolarizing_error  # noqa: E402
 from .sweep import (run_sweep, get_instances, get_single_out,  # noqa: E402
@@ -30,5 +31,6 @@ __all__ = [
     "N_ANCILLA_NOISY_GATES", "QuantumCircuit", "transpile_aer_basis", "AerSimulator",
     "DtcSimulator", "NoiseModel", "depolarizing_error", "run_sweep", "get_instances",
     "get_single_out", "compute_z_expectation", "write_autocorr_csv", "circuit", "aer",
-    "sweep", "distributed", "sharded", "energy", "cli", "energy_cli",
+    "sweep", "distributed", "sharded", "energy", "envelopes", "control", "cli", "energy_cli",
+    "control_cli",
 ]

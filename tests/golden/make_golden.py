@@ -10,6 +10,11 @@ Outputs (committed; the GPU box never reads /root/reference):
                     autocorr_data_L20_circular-polarization/,
                     controlled-autocorr_data_L20/)
   gate_counts.json  every gate_counts_*aer_simulator*.csv (fast.py:193-197)
+  adaptive.json     per-instance adaptive-g histories (g, echo, forward per t) of
+                    autocorr_data_L4/*realtime_adaptive* and
+                    controlled-autocorr_data_L20/*optimization*
+  envelopes.json    series + envelope columns of the *_with_envelopes.csv files
+                    and of the controlled-g optimisation CSV
 Nothing here is source code of the reference: only numeric columns.
 """
 from __future__ import annotations
@@ -102,6 +107,59 @@ def gate_counts():
     return out
 
 
+L4_ADAPT = ("autocorr_data_L4/autocorr_data_vacuum_realtime_adaptive_g0.84_L4_inst1_randomphi1_"
+            "delta0.0_amplitude1.0_noise0.05_usenoise1_target1.0_gain{}.csv")
+L20_OPT = ("controlled-autocorr_data_L20/autocorr_data_vacuum_realtime_adaptive_optimization_"
+           "iter5_g0.84_L20_inst1_randomphi1_delta0.0_amplitude1.0_noise0.05_usenoise1_"
+           "target1.0_gain0.01.csv")
+
+
+def adaptive():
+    out = []
+    for gain in ("0.01", "0.05"):
+        df = pd.read_csv(f"{REF}/{L4_ADAPT.format(gain)}")
+        out.append({"name": f"L4_realtime_gain{gain}", "file": L4_ADAPT.format(gain),
+                    "config": {"L": 4, "g": 0.84, "noise": 0.05, "t_offset": 1,
+                               "target": 1.0, "gain": float(gain), "g_min": 0.84},
+                    "g": df["g_history_inst1"].tolist(),
+                    "echo": df["echo_adaptive_inst1"].tolist(),
+                    "fwd": df["forward_adaptive_inst1"].tolist()})
+    df = pd.read_csv(f"{REF}/{L20_OPT}")
+    out.append({"name": "L20_optimization", "file": L20_OPT, "columns": list(df.columns),
+                "config": {"L": 20, "g": 0.84, "noise": 0.05, "t_offset": 1, "target": 1.0,
+                           "g_min": 0.84, "g_max": 1.0},
+                "g": df["g_history_inst1"].tolist(),
+                "echo": df["echo_adaptive_inst1"].tolist(),
+                "fwd": df["forward_adaptive_inst1"].tolist()})
+    return out
+
+
+def envelopes():
+    out = []
+    pol = glob.glob(f"{REF}/autocorr_data_L20_*polarization/autocorr_data_vacuum_*_pol*_with_envelopes.csv")
+    for path in sorted(pol):
+        df = pd.read_csv(path)
+        rel = os.path.relpath(path, REF)
+        for sig, up, lo in (("av_autocorr", "forward_upper_env", "forward_lower_env"),
+                            ("av_autocorr_echo", "echo_upper_env", "echo_lower_env"),
+                            ("sqrt_av_autocorr_echo", "sqrt_echo_upper_env",
+                             "sqrt_echo_lower_env")):
+            out.append({"file": rel, "variant": "polarization", "window": 3,
+                        "signal": df[sig].tolist(), "upper": df[up].tolist(),
+                        "lower": df[lo].tolist()})
+    df = pd.read_csv(f"{REF}/{L20_OPT}")
+    for sig, tag in (("av_autocorr_adaptive", "adaptive_forward"),
+                     ("av_autocorr_standard_g84", "g84_forward"),
+                     ("av_autocorr_standard_g97", "g97_forward"),
+                     ("av_autocorr_echo_adaptive", "adaptive_echo"),
+                     ("av_autocorr_echo_standard_g84", "g84_echo"),
+                     ("av_autocorr_echo_standard_g97", "g97_echo")):
+        out.append({"file": L20_OPT, "variant": "controlled", "window": 3,
+                    "signal": df[sig].tolist(), "upper": df[f"upper_env_{tag}"].tolist(),
+                    "lower": df[f"lower_env_{tag}"].tolist()})
+    return out
+
+
 def main():
     with open(os.path.join(OUT, "disorder.json"), "w") as f:
         json.dump(disorder(), f, indent=1)
@@ -109,6 +167,10 @@ def main():
         json.dump(aer_autocorr(), f, indent=1)
     with open(os.path.join(OUT, "gate_counts.json"), "w") as f:
         json.dump(gate_counts(), f, indent=0)
+    with open(os.path.join(OUT, "adaptive.json"), "w") as f:
+        json.dump(adaptive(), f, indent=1)
+    with open(os.path.join(OUT, "envelopes.json"), "w") as f:
+        json.dump(envelopes(), f, indent=0)
     print("wrote fixtures to", OUT)
 
 
