@@ -77,7 +77,6 @@ struct dtc_ctx {
   hipStream_t stream = nullptr;
   DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
   bool prof = false;
-  int persist_wgs = 0;  // persistent pass kernels: workgroups per launch (0 = off)
   int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
   double st_ms[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
   double st_bytes[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
@@ -303,6 +302,9 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.diag_stride = rc.pl.diag_stride;
   A.probe = rc.prob->probe_site;
   A.partial = (double*)ctx->partial.p;
+#ifdef DTC_PHASE_TIMING
+  if (const char* e = std::getenv("DTC_DBG_PTR")) A.dbg_ts = (uint64_t*)std::strtoull(e, nullptr, 0);
+#endif
   return A;
 }
 
@@ -342,7 +344,6 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.meas = meas_mode;
   A.meas_at_end = meas_at_end;
   A.batch = batch;
-  A.persist_wgs = ctx->persist_wgs;
   A.n_obs = n_obs;
   const bool has_d = ps.diag != dtc::kDiagNone;
   int shape;
@@ -594,13 +595,6 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   DTC_HIP(hipSetDevice(device));
   dtc_ctx* c = new dtc_ctx();
   c->device = device;
-  // persistent kernels (one workgroup per CU, next tile prefetched) are
-  // opt-in: measured slower than 2 resident workgroups per CU
-  c->persist_wgs = 0;
-  if (const char* e = std::getenv("DTC_PERSISTENT")) {
-    const int v = std::atoi(e);
-    c->persist_wgs = v == 0 ? 0 : (v == 1 ? prop.multiProcessorCount : v);
-  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(DTC_EHIP, "hipStreamCreate failed");

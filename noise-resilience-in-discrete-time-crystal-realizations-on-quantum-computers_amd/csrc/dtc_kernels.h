@@ -66,7 +66,6 @@ struct PassArgs {
   int act;                 // active tile-bit mask (sites kicked by this pass)
   // batch -> (instance, trajectory)
   int batch;               // states in this launch
-  int persist_wgs;         // > 0: persistent launch with this many workgroups
   int64_t batch_start;
   int n_traj;
   int64_t traj_offset;
@@ -92,6 +91,7 @@ struct PassArgs {
   int meas_at_end;         // measure after the post-kick instead of after the diagonal
   int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 2 L_real
   double* partial;         // [B][n_tiles][n_obs]
+  uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
 
 // act must cover nibble sets {2}, {1,2} or {0,1,2}; L_eff in [12, 32].

@@ -47,30 +47,6 @@ __device__ __forceinline__ void bfly_general(double2& u, double2& v, const doubl
   v = nv;
 }
 
-// RX family: [[a, i b], [i c, d]] (a, b, c, d real) — 4 flops per amplitude
-__device__ __forceinline__ void bfly_rx(double2& u, double2& v, double a, double b, double c,
-                                        double d) {
-  double2 nu, nv;
-  nu.x = a * u.x - b * v.y;
-  nu.y = a * u.y + b * v.x;
-  nv.x = d * v.x - c * u.y;
-  nv.y = d * v.y + c * u.x;
-  u = nu;
-  v = nv;
-}
-
-// RY family: [[a, b], [c, d]] real
-__device__ __forceinline__ void bfly_ry(double2& u, double2& v, double a, double b, double c,
-                                        double d) {
-  double2 nu, nv;
-  nu.x = a * u.x + b * v.x;
-  nu.y = a * u.y + b * v.y;
-  nv.x = c * u.x + d * v.x;
-  nv.y = c * u.y + d * v.y;
-  u = nu;
-  v = nv;
-}
-
 // m <- P m for Pauli code (1 X, 2 Y, 3 Z)
 __device__ __forceinline__ void pauli_left(double2* m, int pauli) {
   if (pauli == 1) {
@@ -109,31 +85,54 @@ __device__ __forceinline__ void dagger(double2* m) {
   m[2] = make_double2(m01.x, -m01.y);
 }
 
-// Noisy kick of one site for one layer (see KickMode).
-__device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, uint64_t traj,
-                                double2* m) {
+// Noisy kick of one site for one layer (see KickMode), in two steps so the
+// gate-table loads can be issued before a tile's amplitude loads (vector
+// memory returns in order: a load issued after the tile would make the
+// setup wait for the whole tile).
+static constexpr int kPreSub = 2;  // sub-gates whose tables are loaded up front
+
+__device__ __forceinline__ const double2* kick_gate_ptr(const PassArgs& A, const KickDesc& K,
+                                                        int site, int q) {
+  const int qq = (K.mode == kKickInverse) ? (A.n_sub - 1 - q) : q;
+  return A.kick + (((int64_t)K.row * A.L_kick + site) * A.n_sub + qq) * 4;
+}
+
+__device__ __forceinline__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site,
+                                                uint64_t traj, const double2 (&pre)[kPreSub][4],
+                                                double2* m) {
   m[0] = make_double2(1.0, 0.0);
   m[1] = make_double2(0.0, 0.0);
   m[2] = make_double2(0.0, 0.0);
   m[3] = make_double2(1.0, 0.0);
   const bool inv = (K.mode == kKickInverse);
-  if (A.site_of) site = A.site_of[site];  // sharded state: physical bit -> logical site
   if (K.mode == kKickBasisX) {
     const double r = 0.70710678118654752440;
     m[0] = make_double2(r, 0.0); m[1] = make_double2(r, 0.0);
     m[2] = make_double2(r, 0.0); m[3] = make_double2(-r, 0.0);
     return;
   }
-  for (int q = 0; q < A.n_sub; ++q) {
-    const int qq = inv ? (A.n_sub - 1 - q) : q;
-    const double2* gp = A.kick + (((int64_t)K.row * A.L_kick + site) * A.n_sub + qq) * 4;
-    double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
+  auto apply = [&](int q, double2* gm) {
     if (inv) dagger(gm);
     mat_mul(m, gm, m);
     if (A.noisy) {
       int p = sample_pauli(A.seed, traj, K.stream, K.rng_period, (uint32_t)site, (uint32_t)q,
                            A.thr1, A.thr2, A.thr3);
       pauli_left(m, p);
+    }
+  };
+  if (A.n_sub <= kPreSub) {
+#pragma unroll
+    for (int q = 0; q < kPreSub; ++q) {  // static register indices: no scratch
+      if (q < A.n_sub) {
+        double2 gm[4] = {pre[q][0], pre[q][1], pre[q][2], pre[q][3]};
+        apply(q, gm);
+      }
+    }
+  } else {  // > kPreSub sub-gates per site (generic circuits): reload from the table
+    for (int q = 0; q < A.n_sub; ++q) {
+      const double2* gp = kick_gate_ptr(A, K, site, q);
+      double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
+      apply(q, gm);
     }
   }
   if (K.mode == kKickUndo || K.mode == kKickUndoBasisX) dagger(m);
@@ -145,37 +144,60 @@ __device__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site, 
   }
 }
 
-// Per-site kick of a pass, canonicalised for the pass's matrix family:
-//   RX: M = i^k [[a, i b], [i c, d]]   (Pauli x RX(theta): k = 1 for X errors)
-//   RY: M = i^k [[a, b], [c, d]]       (Pauli x RY(theta): k = 1 for Y errors)
-//   general: M = m (k = 0)
-// The global phases i^k of all sites are multiplied into the diagonal.
+// Per-site kick of a pass, canonicalised for the pass's matrix family.
+// RX family: every unitary i^k [[a, ib], [ic, d]] (a, b, c, d real; Pauli x
+// RX(theta) products, their daggers) has d = sigma a, c = sigma b, sigma = +-1,
+// so  M = i^k * w * diag(1, sigma) * S  with
+//   form A (|a| >= |b|): w = a, S = [[1, i beta], [i beta, 1]],  beta  = b / a
+//   form B (|a| <  |b|): w = b, S = [[alpha, i], [i, alpha]],    alpha = a / b
+// (|coef| <= 1).  S costs 4 FMAs per amplitude pair (2 per amplitude, half of
+// the unfactored butterfly), sigma is a source-negate variant of the same
+// FMAs, and the real scales w of all sites multiply the pass's global phase.
+// RY family: real orthogonal i^k [[a, b], [c, d]] (rotation or reflection):
+// d = sigma a, c = -sigma b,  M = i^k * w * diag(1, sigma) * R,
+//   form A: R = [[1, beta], [-beta, 1]],  form B: R = [[alpha, 1], [-1, alpha]].
+// General kicks (xy, circular, X-basis) keep the full complex 2x2.
 struct SiteMat {
-  double2 m[4];  // general form; RX/RY use m[0].x..m[1].y as a, b, c, d
+  double2 m[4];  // general form
+  double coef;   // RX/RY: beta (form A) or alpha (form B)
+  double scale;  // RX/RY: w
+  int var;       // RX/RY: (form B ? 2 : 0) | (sigma < 0 ? 1 : 0)
   int k;         // power of i
 };
 
 __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat& sm) {
   sm.k = 0;
+  sm.coef = 0.0;
+  sm.scale = 1.0;
+  sm.var = 0;
+  double a, b, c, d;
   if (kind == kKindRX) {
     const bool a_form = (m[0].y == 0.0 && m[1].x == 0.0 && m[2].x == 0.0 && m[3].y == 0.0);
     // B form [[i a, b], [c, i d]] = i [[a, -i b], [-i c, d]]
-    const double a = a_form ? m[0].x : m[0].y;
-    const double b = a_form ? m[1].y : -m[1].x;
-    const double c = a_form ? m[2].y : -m[2].x;
-    const double d = a_form ? m[3].x : m[3].y;
-    sm.m[0] = make_double2(a, b);
-    sm.m[1] = make_double2(c, d);
+    a = a_form ? m[0].x : m[0].y;
+    b = a_form ? m[1].y : -m[1].x;
+    c = a_form ? m[2].y : -m[2].x;
+    d = a_form ? m[3].x : m[3].y;
     sm.k = a_form ? 0 : 1;
   } else if (kind == kKindRY) {
     const bool real = (m[0].y == 0.0 && m[1].y == 0.0 && m[2].y == 0.0 && m[3].y == 0.0);
     // imaginary form i [[a, b], [c, d]]
-    sm.m[0] = make_double2(real ? m[0].x : m[0].y, real ? m[1].x : m[1].y);
-    sm.m[1] = make_double2(real ? m[2].x : m[2].y, real ? m[3].x : m[3].y);
+    a = real ? m[0].x : m[0].y;
+    b = real ? m[1].x : m[1].y;
+    c = real ? m[2].x : m[2].y;
+    d = real ? m[3].x : m[3].y;
     sm.k = real ? 0 : 1;
   } else {
     for (int e = 0; e < 4; ++e) sm.m[e] = m[e];
+    return;
   }
+  // sigma from a d + b c = sigma (a^2 + b^2) (RX) or a d - b c (RY)
+  const double sg = kind == kKindRX ? a * d + b * c : a * d - b * c;
+  const bool neg = sg < 0.0;
+  const bool form_b = fabs(a) < fabs(b);
+  sm.scale = form_b ? b : a;
+  sm.coef = form_b ? a / b : b / a;
+  sm.var = (form_b ? 2 : 0) | (neg ? 1 : 0);
 }
 
 // Tile layouts: register r of lane-thread t holds tile index Y(t, r) =
@@ -206,10 +228,63 @@ __device__ __forceinline__ double uni(double x) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Factored RX-family butterfly (see SiteMat): (u, v) <- diag(1, sigma) S (u, v)
+template <int VAR>
+__device__ __forceinline__ void bfly_rx_f(double2& u, double2& v, double f) {
+  double2 nu, nv;
+  if (VAR == 0) {  // S = [[1, i f], [i f, 1]]
+    nu.x = fma(-f, v.y, u.x); nu.y = fma(f, v.x, u.y);
+    nv.x = fma(-f, u.y, v.x); nv.y = fma(f, u.x, v.y);
+  } else if (VAR == 1) {  // sigma = -1
+    nu.x = fma(-f, v.y, u.x); nu.y = fma(f, v.x, u.y);
+    nv.x = fma(f, u.y, -v.x); nv.y = fma(-f, u.x, -v.y);
+  } else if (VAR == 2) {  // S = [[f, i], [i, f]]
+    nu.x = fma(f, u.x, -v.y); nu.y = fma(f, u.y, v.x);
+    nv.x = fma(f, v.x, -u.y); nv.y = fma(f, v.y, u.x);
+  } else {
+    nu.x = fma(f, u.x, -v.y); nu.y = fma(f, u.y, v.x);
+    nv.x = fma(-f, v.x, u.y); nv.y = fma(-f, v.y, -u.x);
+  }
+  u = nu;
+  v = nv;
+}
+
+// Factored RY-family butterfly: (u, v) <- diag(1, sigma) R (u, v)
+template <int VAR>
+__device__ __forceinline__ void bfly_ry_f(double2& u, double2& v, double f) {
+  double2 nu, nv;
+  if (VAR == 0) {  // R = [[1, f], [-f, 1]]
+    nu.x = fma(f, v.x, u.x); nu.y = fma(f, v.y, u.y);
+    nv.x = fma(-f, u.x, v.x); nv.y = fma(-f, u.y, v.y);
+  } else if (VAR == 1) {
+    nu.x = fma(f, v.x, u.x); nu.y = fma(f, v.y, u.y);
+    nv.x = fma(f, u.x, -v.x); nv.y = fma(f, u.y, -v.y);
+  } else if (VAR == 2) {  // R = [[f, 1], [-1, f]]
+    nu.x = fma(f, u.x, v.x); nu.y = fma(f, u.y, v.y);
+    nv.x = fma(f, v.x, -u.x); nv.y = fma(f, v.y, -u.y);
+  } else {
+    nu.x = fma(f, u.x, v.x); nu.y = fma(f, u.y, v.y);
+    nv.x = fma(-f, v.x, u.x); nv.y = fma(-f, v.y, u.y);
+  }
+  u = nu;
+  v = nv;
+}
+
+template <int KIND, int VAR, int Q>
+__device__ __forceinline__ void layer_f(double2 (&v)[kRegs], double f) {
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    if (r & (1 << Q)) continue;
+    if (KIND == kKindRX) bfly_rx_f<VAR>(v[r], v[r | (1 << Q)], f);
+    else bfly_ry_f<VAR>(v[r], v[r | (1 << Q)], f);
+  }
+}
+
 template <int N, int KIND>
 __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const SiteMat* s_mat, int act) {
   // Every site of an active nibble runs (inactive sites carry the identity):
-  // no data-dependent branches, so no register shuffles at merge points.
+  // no data-dependent branches, so no register shuffles at merge points; the
+  // RX/RY variant branch is wave-uniform.
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int k = 4 * N + q;
@@ -226,14 +301,19 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const SiteMat*
         for (int r = 0; r < kRegs; ++r)
           if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
       } else {
-        const double a = uni(s_mat[k].m[0].x), b = uni(s_mat[k].m[0].y);
-        const double c = uni(s_mat[k].m[1].x), d = uni(s_mat[k].m[1].y);
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-          if (r & (1 << q)) continue;
-          if (KIND == kKindRX) bfly_rx(v[r], v[r | (1 << q)], a, b, c, d);
-          else bfly_ry(v[r], v[r | (1 << q)], a, b, c, d);
-        }
+        const double f = uni(s_mat[k].coef);
+        const int var = __builtin_amdgcn_readfirstlane(s_mat[k].var);
+        auto run = [&](auto qtag) {
+          constexpr int Q = decltype(qtag)::value;
+          if (var == 0) layer_f<KIND, 0, Q>(v, f);
+          else if (var == 1) layer_f<KIND, 1, Q>(v, f);
+          else if (var == 2) layer_f<KIND, 2, Q>(v, f);
+          else layer_f<KIND, 3, Q>(v, f);
+        };
+        if (q == 0) run(std::integral_constant<int, 0>{});
+        else if (q == 1) run(std::integral_constant<int, 1>{});
+        else if (q == 2) run(std::integral_constant<int, 2>{});
+        else run(std::integral_constant<int, 3>{});
       }
     }
   }
@@ -292,15 +372,28 @@ struct RoundPlan {
   static constexpr int p2 = n2 ? 2 : p0;
 };
 
-template <int SHAPE, int NIBS, int KIND, bool PERSIST>
+// Development-only phase timing (build with -DDTC_PHASE_TIMING): wave 0 of
+// every workgroup records s_memtime at phase boundaries into A.dbg_ts.
+#ifdef DTC_PHASE_TIMING
+#define DTC_TS(i) (ts[i] = __builtin_amdgcn_s_memtime())
+#else
+#define DTC_TS(i) ((void)0)
+#endif
+
+template <int SHAPE, int NIBS, int KIND>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
+#ifdef DTC_PHASE_TIMING
+  uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  DTC_TS(0);
   __shared__ double2 s_tile[kTile];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
   __shared__ SiteMat s_pre[RP::pre ? kTileBits : 1];
   __shared__ SiteMat s_post[RP::post ? kTileBits : 1];
-  __shared__ int s_k[2 * kTileBits];
+  __shared__ int s_kc[2];
+  __shared__ double s_w[2];
   __shared__ double s_red[kThreads / 64][kMaxObs];
 
   const int t = threadIdx.x;
@@ -308,264 +401,283 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const int c = A.c, s = A.s;
   const int tile_bits = A.L_eff - kTileBits;
   const int64_t n_tiles = (int64_t)1 << tile_bits;
-
-  // work: tile indices idx = state * n_tiles + tile.  Non-persistent: one tile
-  // per workgroup.  Persistent: a contiguous range per workgroup (tiles of one
-  // state stay together, so kick matrices are rebuilt only when the state
-  // changes), with the next tile's loads in flight during this tile's rounds.
-  int64_t first, last;
-  if (PERSIST) {
-    const int64_t total = n_tiles * A.batch;
-    const int64_t per = (total + gridDim.x - 1) / gridDim.x;
-    first = (int64_t)blockIdx.x * per;
-    last = first + per < total ? first + per : total;
-  } else {
-    first = (int64_t)blockIdx.y * n_tiles + blockIdx.x;
-    last = first + 1;
-  }
-  if (first >= last) return;
+  const int64_t b = blockIdx.y;
+  const int64_t tile = blockIdx.x;
+  const int64_t gstate = A.batch_start + b;
+  const int inst = (int)(gstate / A.n_traj);
+  const uint64_t traj = (uint64_t)(A.traj_offset + (gstate % A.n_traj));
 
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
   M.c = c;
   M.s = s;
   M.cmask = (1 << c) - 1;
-  auto tile_base = [&](int64_t idx) -> int64_t {
-    const int64_t tile = idx & (n_tiles - 1);
-    return ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
-  };
-  // Address = uniform 64-bit base (state + tile base + register offset, SGPRs)
-  // + one per-lane 32-bit byte offset shared by all 16 accesses (L_eff <= 32).
+  M.tbase = ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
+
+  // ---- phase 1: the setup's global loads (kick gates of this thread's site,
+  // diagonal tables of the state's instance), issued before the tile ----
+  const bool is_pre = RP::pre && t < kTileBits;
+  const bool is_post = RP::post && t >= 64 && t < 64 + kTileBits;
+  const int k = is_pre ? t : t - 64;
+  const KickDesc& K = is_pre ? A.pre : A.post;
+  int site = 0;
+  bool kick_on = false;
+  double2 gpre[kPreSub][4];
+  if (is_pre || is_post) {
+    const int lsite = k < c ? k : s + k - c;
+    kick_on = (act & ~(int)K.skip & (1 << k)) && lsite < A.L_real;
+    if (kick_on) {
+      site = A.site_of ? A.site_of[lsite] : lsite;  // sharded: physical bit -> logical site
+      if (K.mode != kKickBasisX) {
+#pragma unroll
+        for (int q = 0; q < kPreSub; ++q) {
+          if (q < A.n_sub) {
+            const double2* gp = kick_gate_ptr(A, K, site, q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gpre[q][e] = gp[e];
+          }
+        }
+      }
+    }
+  }
+  constexpr int kChunkPerThread = (kMaxChunks * 64 + kThreads - 1) / kThreads;
+  double2 dchunk[kChunkPerThread];
+  double2 dwin = make_double2(1.0, 0.0);
+  int g0 = -1;
+  if (RP::diag) {
+    const int tb = 4 * RP::d_lay;
+    g0 = tb >= c ? s + tb - c : (tb + 4 <= c ? tb : -1);
+    const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
+#pragma unroll
+    for (int j = 0; j < kChunkPerThread; ++j) {
+      const int i = t + j * kThreads;
+      if (i < A.n_chunks * 64) dchunk[j] = dt[i];
+    }
+    if (g0 >= 0 && t < 64) dwin = dt[(A.n_chunks + g0) * 64 + t];
+  }
+
+  // ---- phase 2: the tile (coalesced 16-B loads: uniform 64-bit base +
+  // one per-lane 32-bit byte offset shared by all 16 accesses, L_eff <= 32) ----
   const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
-  double2 vn[kRegs];
-  auto load_tile = [&](int64_t idx) {
-    const char* src = (const char*)(A.src + (idx >> tile_bits) * A.state_len);
-    const int64_t tb = tile_base(idx);
+  double2 v[kRegs];
+  {
+    const char* src = (const char*)(A.src + b * A.state_len);
 #pragma unroll
     for (int r = 0; r < kRegs; ++r)
-      vn[r] = *(const double2*)(src + ((tb | M.rel(r << 8)) << 4) + vofs);
-  };
-  load_tile(first);
+      v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
+  }
+  // vmcnt(16) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt/lgkmcnt
+  // unmasked): the setup loads have landed, the tile's 16 are still in flight.
+  // Explicit, so the divergent setup code below never waits for the tile.
+  static_assert(kRegs == 16, "vmcnt immediate assumes 16 tile loads");
+  __builtin_amdgcn_s_waitcnt(0x4F70);
+  DTC_TS(1);
 
-  int64_t cur_state = -1;
-  double2 gph = make_double2(1.0, 0.0);
-  int g0 = -1;
-
-  for (int64_t idx = first; idx < last; ++idx) {
-    double2 v[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = vn[r];
-    if (PERSIST && idx + 1 < last) load_tile(idx + 1);
-    const int64_t b = idx >> tile_bits;
-    const int64_t tile = idx & (n_tiles - 1);
-    M.tbase = tile_base(idx);
-
-    if (b != cur_state) {
-      // ---- per-state setup: kick matrices (threads 0..11 pre, 64..75 post),
-      // their global phase, diagonal tables of the state's instance ----
-      cur_state = b;
-      const int64_t g = A.batch_start + b;
-      const int inst = (int)(g / A.n_traj);
-      const uint64_t traj = (uint64_t)(A.traj_offset + (g % A.n_traj));
-      if (PERSIST) __syncthreads();  // previous tile done with s_pre/s_post/tables
-      {
-        const bool is_pre = t < kTileBits;
-        const bool is_post = t >= 64 && t < 64 + kTileBits;
-        const int k = is_pre ? t : t - 64;
-        int kk = 0;
-        if ((is_pre && RP::pre) || (is_post && RP::post)) {
-          const KickDesc K = is_pre ? A.pre : A.post;
-          const int site = k < c ? k : s + k - c;
-          double2 m[4];
-          if ((act & ~(int)K.skip & (1 << k)) && site < A.L_real) {
-            build_site_kick(A, K, site, traj, m);
-          } else {  // inactive tile bits and padding sites: identity
-            m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
-            m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
-          }
-          SiteMat sm;
-          canonicalise(KIND, m, sm);
-          if (is_pre) s_pre[k] = sm;
-          else s_post[k] = sm;
-          kk = sm.k;
-        }
-        if (is_pre) s_k[k] = kk;
-        if (is_post) s_k[kTileBits + k] = kk;
+  // ---- phase 3: setup compute while the tile is in flight: noisy kick
+  // matrices (threads 0..11 pre, 64..75 post), their global phase, tables ----
+  {
+    int kk = 0;
+    double wscale = 1.0;
+    if (is_pre || is_post) {
+      double2 m[4];
+      if (kick_on) {
+        build_site_kick(A, K, site, traj, gpre, m);
+      } else {  // inactive tile bits and padding sites: identity
+        m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
+        m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
       }
-      // diagonal tables: chunk tables + the window table of the layout the
-      // diagonal is applied in (registers = 4 contiguous global bits [g0, g0+4))
-      if (RP::diag) {
-        const int tb = 4 * RP::d_lay;
-        g0 = tb >= c ? s + tb - c : (tb + 4 <= c ? tb : -1);
-        const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
-        const double cs = A.diag_conj ? -1.0 : 1.0;
-        for (int i = t; i < A.n_chunks * 64; i += kThreads) {
-          const double2 e = dt[i];
-          s_chunk[i] = make_double2(e.x, cs * e.y);
-        }
-        if (g0 >= 0 && t < 64) {
-          const double2 e = dt[(A.n_chunks + g0) * 64 + t];
-          s_win[t] = make_double2(e.x, cs * e.y);
-        }
-      }
-      __syncthreads();  // matrices, phases and tables ready
-      // global phase i^k of the canonicalised kicks of this pass
-      int ksum = 0;
-      for (int i = 0; i < 2 * kTileBits; ++i) ksum += s_k[i];
-      const int kph = __builtin_amdgcn_readfirstlane(ksum) & 3;
-      gph = make_double2(kph == 0 ? 1.0 : (kph == 2 ? -1.0 : 0.0),
-                         kph == 1 ? 1.0 : (kph == 3 ? -1.0 : 0.0));
+      SiteMat sm;
+      canonicalise(KIND, m, sm);
+      if (is_pre) s_pre[k] = sm;
+      else s_post[k] = sm;
+      kk = sm.k;
+      wscale = sm.scale;
     }
+    // i^k phases: k is 0 or 1 per site; waves 0 (pre) and 1 (post) count them
+    // and multiply the sites' real scales w
+    const unsigned long long bal = __ballot(kk != 0);
+    double w = wscale;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) w *= __shfl_xor(w, off, 64);
+    if (t == 0) { s_kc[0] = __popcll(bal); s_w[0] = w; }
+    if (t == 64) { s_kc[1] = __popcll(bal); s_w[1] = w; }
+    if (RP::diag) {
+      const double cs = A.diag_conj ? -1.0 : 1.0;
+#pragma unroll
+      for (int j = 0; j < kChunkPerThread; ++j) {
+        const int i = t + j * kThreads;
+        if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
+      }
+      if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    }
+  }
+  __syncthreads();  // matrices, phases and tables ready
+  DTC_TS(2);
+  const int kph = __builtin_amdgcn_readfirstlane(s_kc[0] + s_kc[1]) & 3;
+  // global factor of the factored kicks, i^k * w_pre * w_post, applied with
+  // the diagonal (the state's arithmetic does not depend on whether it is
+  // measured; a measurement between the diagonal and the post-kick divides
+  // its sums by w_post^2)
+  const double w_post = RP::post ? s_w[1] : 1.0;
+  const double wg = (RP::pre ? s_w[0] : 1.0) * w_post;
+  const double2 gph = make_double2(kph == 0 ? wg : (kph == 2 ? -wg : 0.0),
+                                   kph == 1 ? wg : (kph == 3 ? -wg : 0.0));
 
-    auto diag_in = [&](auto lay_tag) {
-      constexpr int LAY = decltype(lay_tag)::value;
-      const int64_t x0 = M.at(ybase<LAY>(t));
-      if (g0 >= 0) {
-        // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
-        // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
-        // complex products per amplitude
-        const int w0i = (int)(((x0 << 1) >> g0) & 63);
-        const double2 w0 = s_win[w0i];
-        const double2 pc =
-            cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+  auto diag_in = [&](auto lay_tag) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int64_t x0 = M.at(ybase<LAY>(t));
+    if (g0 >= 0) {
+      // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
+      // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
+      // complex products per amplitude
+      const int w0i = (int)(((x0 << 1) >> g0) & 63);
+      const double2 w0 = s_win[w0i];
+      const double2 pc =
+          cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
-      } else {
+      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
+    } else {
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r)
-          v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
-                                                 x0 | M.rel(r << (4 * LAY)))));
-      }
+      for (int r = 0; r < kRegs; ++r)
+        v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
+                                               x0 | M.rel(r << (4 * LAY)))));
+    }
+  };
+  // Observables of the tile: (sum |a|^2, sum z_i |a|^2 for the probe or every
+  // site).  Only sites inside the tile need a reduction: a register bit of the
+  // layout from per-thread partial sums, a thread bit from the signed thread
+  // total; a site outside the tile has one sign over the tile (tbase).
+  auto measure_in = [&](auto lay_tag, double inv_w2) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int64_t x0 = M.at(ybase<LAY>(t));
+    const int wave = t >> 6, lane = t & 63;
+    double pr[kRegs];
+    double ptot = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
+      ptot += pr[r];
+    }
+    double zr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double z = 0.0;
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
+      zr[j] = z;
+    }
+    double tot = wave_sum(ptot);
+    if (lane == 0) s_red[wave][0] = tot;
+    const bool probe_only = A.meas == kMeasProbe;
+    const int n_z = probe_only ? 1 : A.L_real;
+    auto tile_bit = [&](int site) {
+      return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
-    // Observables of the tile: (sum |a|^2, sum z_i |a|^2 for the probe or every
-    // site).  Only sites inside the tile need a reduction: a register bit of the
-    // layout from per-thread partial sums, a thread bit from the signed thread
-    // total; a site outside the tile has one sign over the tile (tbase).
-    auto measure_in = [&](auto lay_tag) {
-      constexpr int LAY = decltype(lay_tag)::value;
-      const int64_t x0 = M.at(ybase<LAY>(t));
-      const int wave = t >> 6, lane = t & 63;
-      double pr[kRegs];
-      double ptot = 0.0;
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) {
-        pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
-        ptot += pr[r];
-      }
-      double zr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
+    for (int i = 0; i < n_z; ++i) {
+      const int site = probe_only ? A.probe : i;
+      const int tb = tile_bit(site);
+      if (tb < 0) continue;
+      const int j = tb - 4 * LAY;
+      double z;
+      if (j >= 0 && j < 4)
+        z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
+      else
+        z = ((x0 >> site) & 1) ? -ptot : ptot;
+      z = wave_sum(z);
+      if (lane == 0) s_red[wave][1 + i] = z;
+    }
+    if (A.meas == kMeasEnergy) {
+      // bond correlators <Z_i Z_i+1>: sign per amplitude, generic reduction
+      for (int i = 0; i + 1 < A.L_real; ++i) {
         double z = 0.0;
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
-        zr[j] = z;
-      }
-      double tot = wave_sum(ptot);
-      if (PERSIST) __syncthreads();  // s_red of the previous tile consumed
-      if (lane == 0) s_red[wave][0] = tot;
-      const bool probe_only = A.meas == kMeasProbe;
-      const int n_z = probe_only ? 1 : A.L_real;
-      auto tile_bit = [&](int site) {
-        return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
-      };
-      for (int i = 0; i < n_z; ++i) {
-        const int site = probe_only ? A.probe : i;
-        const int tb = tile_bit(site);
-        if (tb < 0) continue;
-        const int j = tb - 4 * LAY;
-        double z;
-        if (j >= 0 && j < 4)
-          z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
-        else
-          z = ((x0 >> site) & 1) ? -ptot : ptot;
-        z = wave_sum(z);
-        if (lane == 0) s_red[wave][1 + i] = z;
-      }
-      if (A.meas == kMeasEnergy) {
-        // bond correlators <Z_i Z_i+1>: sign per amplitude, generic reduction
-        for (int i = 0; i + 1 < A.L_real; ++i) {
-          double z = 0.0;
-#pragma unroll
-          for (int r = 0; r < kRegs; ++r) {
-            const int64_t x = x0 | M.rel(r << (4 * LAY));
-            z += (((x >> i) ^ (x >> (i + 1))) & 1) ? -pr[r] : pr[r];
-          }
-          z = wave_sum(z);
-          if (lane == 0) s_red[wave][1 + A.L_real + i] = z;
+        for (int r = 0; r < kRegs; ++r) {
+          const int64_t x = x0 | M.rel(r << (4 * LAY));
+          z += (((x >> i) ^ (x >> (i + 1))) & 1) ? -pr[r] : pr[r];
         }
+        z = wave_sum(z);
+        if (lane == 0) s_red[wave][1 + A.L_real + i] = z;
       }
-      __syncthreads();
-      if (t < A.n_obs) {
-        const int site = probe_only ? A.probe : t - 1;
-        const bool is_site = t >= 1 && t <= n_z;
-        const int ws = (!is_site || tile_bit(site) >= 0) ? t : 0;
-        double acc = 0.0;
-        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
-        if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
-        A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
-      }
-    };
-    using IC2 = std::integral_constant<int, 2>;
+    }
+    __syncthreads();
+    if (t < A.n_obs) {
+      const int site = probe_only ? A.probe : t - 1;
+      const bool is_site = t >= 1 && t <= n_z;
+      const int ws = (!is_site || tile_bit(site) >= 0) ? t : 0;
+      double acc = 0.0;
+      for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
+      if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
+      acc *= inv_w2;
+      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    }
+  };
+  using IC2 = std::integral_constant<int, 2>;
 
-    // ---- pre-kick rounds: 2 -> 0 -> 1 ----
-    if constexpr (RP::pre) {
-      if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
-      if constexpr (RP::n0) {
-        exchange<2, 0>(v, s_tile, t);
-        apply_nibble<0, KIND>(v, s_pre, act);
-      }
-      if constexpr (RP::n1) {
-        exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
-        apply_nibble<1, KIND>(v, s_pre, act);
-      }
+  // ---- pre-kick rounds: 2 -> 0 -> 1 ----
+  if constexpr (RP::pre) {
+    if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
+    if constexpr (RP::n0) {
+      exchange<2, 0>(v, s_tile, t);
+      apply_nibble<0, KIND>(v, s_pre, act);
     }
-    // ---- diagonal and measurement at d_lay ----
-    using DL = std::integral_constant<int, RP::d_lay>;
-    if constexpr (RP::diag) diag_in(DL{});
-    if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{});
-    // ---- post-kick rounds: 1 -> 0 -> 2 ----
-    if constexpr (RP::post) {
-      if constexpr (RP::n1) {
-        exchange<RP::d_lay, 1>(v, s_tile, t);
-        apply_nibble<1, KIND>(v, s_post, act);
-      }
-      if constexpr (RP::n0) {
-        exchange<RP::p1, 0>(v, s_tile, t);
-        apply_nibble<0, KIND>(v, s_post, act);
-      }
-      if constexpr (RP::n2) {
-        exchange<RP::p0, 2>(v, s_tile, t);
-        apply_nibble<2, KIND>(v, s_post, act);
-      }
-      exchange<RP::p2, 2>(v, s_tile, t);
-    } else {
-      exchange<RP::d_lay, 2>(v, s_tile, t);
+    if constexpr (RP::n1) {
+      exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
+      apply_nibble<1, KIND>(v, s_pre, act);
     }
-    if constexpr (!RP::diag) {
-      // no diagonal to carry the kicks' global phase
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
-    }
-    if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{});
-
-    char* dst = (char*)(A.dst + b * A.state_len);
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r)
-      *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
   }
+  DTC_TS(3);
+  if constexpr (!RP::diag) {
+    // no diagonal to carry the kicks' global factor (kick-only pass: no
+    // post-kick, so applying it here, before any measurement, is exact)
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
+  }
+  // ---- diagonal and measurement at d_lay ----
+  using DL = std::integral_constant<int, RP::d_lay>;
+  if constexpr (RP::diag) diag_in(DL{});
+  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{}, 1.0 / (w_post * w_post));  // before the post-kick
+  DTC_TS(4);
+  // ---- post-kick rounds: 1 -> 0 -> 2 ----
+  if constexpr (RP::post) {
+    if constexpr (RP::n1) {
+      exchange<RP::d_lay, 1>(v, s_tile, t);
+      apply_nibble<1, KIND>(v, s_post, act);
+    }
+    if constexpr (RP::n0) {
+      exchange<RP::p1, 0>(v, s_tile, t);
+      apply_nibble<0, KIND>(v, s_post, act);
+    }
+    if constexpr (RP::n2) {
+      exchange<RP::p0, 2>(v, s_tile, t);
+      apply_nibble<2, KIND>(v, s_post, act);
+    }
+    exchange<RP::p2, 2>(v, s_tile, t);
+  } else {
+    exchange<RP::d_lay, 2>(v, s_tile, t);
+  }
+  if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{}, 1.0);
+  DTC_TS(5);
+
+  char* dst = (char*)(A.dst + b * A.state_len);
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r)
+    *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+#ifdef DTC_PHASE_TIMING
+  DTC_TS(6);
+  if (A.dbg_ts && t < 8 && SHAPE == DTC_PHASE_TIMING) {
+    // t 0..6: phase stamps (s_memtime); 7: HW_ID (CU/SIMD/XCC placement)
+    const uint64_t val = t < 7 ? ts[t & 7] : (uint64_t)__builtin_amdgcn_s_getreg(
+                                                 (4 << 0) | (0 << 6) | (31 << 11));
+    A.dbg_ts[(b * n_tiles + tile) * 8 + t] = val | ((uint64_t)NIBS << 60);
+  }
+#endif
 }
 
-// Kernel symbols per pass shape so rocprofv3 traces separate them.  The
-// persistent variants (1 workgroup per CU, next tile prefetched into
-// registers) carry a _p suffix.
+// Kernel symbols per pass shape so rocprofv3 traces separate them.
 #define DTC_DEFINE_PASS(NAME, SHAPE_EXPR)                                          \
   template <int NIBS, int KIND>                                                    \
   __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
-    pass_body<SHAPE_EXPR, NIBS, KIND, false>(A);                                   \
-  }                                                                                \
-  template <int NIBS, int KIND>                                                    \
-  __global__ __launch_bounds__(kThreads, 1) void NAME##_p(PassArgs A) {            \
-    pass_body<SHAPE_EXPR, NIBS, KIND, true>(A);                                    \
+    pass_body<SHAPE_EXPR, NIBS, KIND>(A);                                          \
   }
 DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
@@ -574,24 +686,12 @@ DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
 #undef DTC_DEFINE_PASS
 template <int NIBS>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
-  pass_body<kShapeD, NIBS, kKindRX, false>(A);
+  pass_body<kShapeD, NIBS, kKindRX>(A);
 }
 
 template <int NIBS, int KIND>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
-  if (a.persist_wgs > 0) {
-    dim3 pg(a.persist_wgs);
-    switch (shape) {
-      case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
-      case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
-      case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
-      case kShapeK: hipLaunchKernelGGL((dtc_kick_pass_p<NIBS, KIND>), pg, block, 0, stream, a); break;
-      case kShapeD: hipLaunchKernelGGL((dtc_diag_pass<NIBS>), grid, block, 0, stream, a); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
   switch (shape) {
     case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
     case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
@@ -614,7 +714,9 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, hipStr
 }
 
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream) {
-  if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch) return hipErrorInvalidValue;
+  if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch || batch > 65535 ||
+      a.n_chunks > kMaxChunks)
+    return hipErrorInvalidValue;
   const int n_tiles = 1 << (a.L_eff - kTileBits);
   dim3 grid(n_tiles, batch);
   int nibs = 0;
