@@ -76,6 +76,8 @@ struct dtc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
+  DevBuf recs, recs1, pk;               // kick records (batch schedule / single pass), pass list
+  std::vector<dtc::PassKick> pk_host;   // staged pass list (alive until the stream syncs)
   bool prof = false;
   int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
   double st_ms[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
@@ -285,18 +287,8 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.state_len = rc.pl.len;
   A.L_eff = rc.pl.L_eff;
   A.L_real = rc.pl.L;
-  A.L_kick = rc.prob->L;
-  A.site_of = rc.site_of;
   A.batch_start = batch_start;
   A.n_traj = rc.n_traj;
-  A.traj_offset = rc.traj_offset;
-  A.kick = (const double2*)ctx->kick.p;
-  A.n_sub = rc.prob->n_sub;
-  A.thr1 = rc.thr1;
-  A.thr2 = rc.thr2;
-  A.thr3 = rc.thr3;
-  A.seed = rc.seed;
-  A.noisy = rc.noisy;
   A.diag = (const double2*)ctx->diag.p;
   A.n_chunks = rc.pl.n_chunks;
   A.diag_stride = rc.pl.diag_stride;
@@ -306,6 +298,25 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   if (const char* e = std::getenv("DTC_DBG_PTR")) A.dbg_ts = (uint64_t*)std::strtoull(e, nullptr, 0);
 #endif
   return A;
+}
+
+dtc::PrepArgs prep_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch) {
+  dtc::PrepArgs P{};
+  P.batch = batch;
+  P.batch_start = batch_start;
+  P.n_traj = rc.n_traj;
+  P.traj_offset = rc.traj_offset;
+  P.kick = (const double2*)ctx->kick.p;
+  P.n_sub = rc.prob->n_sub;
+  P.L_kick = rc.prob->L;
+  P.L_real = rc.pl.L;
+  P.site_of = rc.site_of;
+  P.thr1 = rc.thr1;
+  P.thr2 = rc.thr2;
+  P.thr3 = rc.thr3;
+  P.seed = rc.seed;
+  P.noisy = rc.noisy;
+  return P;
 }
 
 int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* out,
@@ -326,10 +337,60 @@ int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* 
   return DTC_OK;
 }
 
-// Launch one pass; if meas_mode != none, reduce its observables into meas_out.
+// Shape and matrix family of a pass.
+int pass_shape(const PassSpec& ps) {
+  const bool has_d = ps.diag != dtc::kDiagNone;
+  if (ps.pre.enabled && has_d && ps.post.enabled) return dtc::kShapeKDK;
+  if (ps.pre.enabled && has_d) return dtc::kShapeKD;
+  if (has_d && ps.post.enabled) return dtc::kShapeDK;
+  if (ps.pre.enabled && !has_d && !ps.post.enabled) return dtc::kShapeK;
+  if (has_d) return dtc::kShapeD;
+  return -1;
+}
+
+int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
+  int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
+  for (const KickDesc* k : {&ps.pre, &ps.post}) {
+    if (!k->enabled) continue;
+    const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
+    const int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
+    kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
+  }
+  return kind;
+}
+
+dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
+  const Group& g = rc.pl.groups[ps.group];
+  dtc::PassKick pk{};
+  pk.pre = ps.pre;
+  pk.post = ps.post;
+  pk.kind = pass_kind(rc, ps, pass_shape(ps));
+  pk.c = g.c;
+  pk.s = g.s;
+  pk.act = g.act;
+  return pk;
+}
+
+// Launch one pass whose kick records are `recs` ([batch][kRecPerState]; null:
+// build them first with a one-pass prep launch); if meas_mode != none, reduce
+// its observables into meas_out.
 int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
-                     int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride) {
+                     int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
+                     const dtc::KickRec* recs = nullptr) {
+  const int shape = pass_shape(ps);
+  if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
+  const int kind = pass_kind(rc, ps, shape);
+  if (!recs) {
+    DTC_TRY(ensure(ctx->recs1, (size_t)batch * dtc::kRecPerState * sizeof(dtc::KickRec)));
+    dtc::PrepArgs P = prep_args(ctx, rc, batch_start, batch);
+    P.passes = nullptr;
+    P.one = pass_kick(rc, ps);
+    P.n_pass = 1;
+    P.out = (dtc::KickRec*)ctx->recs1.p;
+    DTC_HIP(dtc::launch_prep(P, ctx->stream));
+    recs = P.out;
+  }
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
   const Group& g = rc.pl.groups[ps.group];
   A.src = src;
@@ -338,29 +399,13 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.s = g.s;
   A.tile_bits_mid = g.s - g.c;
   A.act = g.act;
-  A.pre = ps.pre;
-  A.post = ps.post;
+  A.recs = recs;
   A.diag_conj = ps.diag == dtc::kDiagConj;
   A.meas = meas_mode;
   A.meas_at_end = meas_at_end;
   A.batch = batch;
   A.n_obs = n_obs;
-  const bool has_d = ps.diag != dtc::kDiagNone;
-  int shape;
-  if (ps.pre.enabled && has_d && ps.post.enabled) shape = dtc::kShapeKDK;
-  else if (ps.pre.enabled && has_d) shape = dtc::kShapeKD;
-  else if (has_d && ps.post.enabled) shape = dtc::kShapeDK;
-  else if (ps.pre.enabled && !has_d && !ps.post.enabled) shape = dtc::kShapeK;
-  else if (has_d) shape = dtc::kShapeD;
-  else return fail(DTC_EINVAL, "internal: empty pass");
-  int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
-  for (const KickDesc* k : {&ps.pre, &ps.post}) {
-    if (!k->enabled) continue;
-    const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
-    const int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
-    kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
-  }
-  const int kernel = has_d ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
+  const int kernel = ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->prof) {
     e0 = get_event(ctx);
@@ -374,6 +419,45 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   }
   if (meas_mode != dtc::kMeasNone)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
+  return DTC_OK;
+}
+
+// A scheduled pass of a batch (dtc_autocorr builds the whole batch schedule,
+// prepares every kick record with one prep launch per segment, then streams
+// the passes).
+struct Launch {
+  PassSpec ps;
+  const double2* src;
+  double2* dst;
+  int meas_mode, meas_at_end, n_obs;
+  double* meas_out;
+  int64_t meas_stride;
+};
+
+int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
+                 const std::vector<Launch>& L) {
+  const size_t per_pass = (size_t)batch * dtc::kRecPerState * sizeof(dtc::KickRec);
+  const size_t seg = std::max<size_t>(1, std::min<size_t>(L.size(), (size_t)(256u << 20) / per_pass));
+  DTC_TRY(ensure(ctx->recs, seg * per_pass));
+  ctx->pk_host.resize(L.size());
+  for (size_t i = 0; i < L.size(); ++i) ctx->pk_host[i] = pass_kick(rc, L[i].ps);
+  DTC_TRY(ensure(ctx->pk, L.size() * sizeof(dtc::PassKick)));
+  DTC_HIP(hipMemcpyAsync(ctx->pk.p, ctx->pk_host.data(), L.size() * sizeof(dtc::PassKick),
+                         hipMemcpyHostToDevice, ctx->stream));
+  for (size_t i0 = 0; i0 < L.size(); i0 += seg) {
+    const size_t n = std::min(seg, L.size() - i0);
+    dtc::PrepArgs P = prep_args(ctx, rc, batch_start, batch);
+    P.passes = (const dtc::PassKick*)ctx->pk.p + i0;
+    P.n_pass = (int)n;
+    P.out = (dtc::KickRec*)ctx->recs.p;
+    DTC_HIP(dtc::launch_prep(P, ctx->stream));
+    for (size_t i = 0; i < n; ++i) {
+      const Launch& l = L[i0 + i];
+      DTC_TRY(launch_pass_spec(ctx, rc, batch_start, batch, l.ps, l.src, l.dst, l.meas_mode,
+                               l.meas_at_end, l.n_obs, l.meas_out, l.meas_stride,
+                               P.out + i * batch * dtc::kRecPerState));
+    }
+  }
   return DTC_OK;
 }
 
@@ -621,6 +705,9 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->kick);
   release(ctx->basis);
   release(ctx->sitemap);
+  release(ctx->recs);
+  release(ctx->recs1);
+  release(ctx->pk);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return DTC_OK;
@@ -755,7 +842,8 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
                              ctx->stream));
 
     // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
-    // and branch the echo at t off F.
+    // and branch the echo at t off F.  The whole batch schedule is built first.
+    std::vector<Launch> sched;
     if (P > 0) {
       Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
       while (!fw.done()) {
@@ -764,18 +852,25 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
         const int t = p - pr->t_offset;
         const bool closes = ps.diag != dtc::kDiagNone;
         const bool meas = closes && want_f && t >= 0 && t >= pr->t_first;
-        DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, ps, F, F, meas ? meas_f : dtc::kMeasNone, 0,
-                                 n_obs_f,
-                                 meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
-                                 (int64_t)T * n_obs_f));
+        sched.push_back(Launch{ps, F, F, meas ? meas_f : dtc::kMeasNone, 0, n_obs_f,
+                               meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
+                               (int64_t)T * n_obs_f});
         if (!closes || !want_e || t < 0 || t < pr->t_first) continue;
         std::vector<int> ahead(pl.groups.size());
         for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > p;
         Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
-        DTC_TRY(run_chain(ctx, rc, bs, nb, ec, F, E, dtc::kMeasProbe, 2,
-                          (double*)ctx->vals_e.p + (size_t)t * 2, (int64_t)T * 2));
+        const double2* src = F;
+        while (!ec.done()) {
+          PassSpec es = next_pass(ec);
+          const bool last = ec.done();
+          sched.push_back(Launch{es, src, E, last ? dtc::kMeasProbe : dtc::kMeasNone, 1, 2,
+                                 last ? (double*)ctx->vals_e.p + (size_t)t * 2 : nullptr,
+                                 (int64_t)T * 2});
+          src = E;
+        }
       }
     }
+    DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
     if (want_e)

@@ -48,6 +48,47 @@ struct KickDesc {
   uint32_t skip;        // tile bits of the pass left unkicked (identity); 0 = none
 };
 
+// Kick records.  Every noisy kick of a pass is a pure function of (pass,
+// state, site): the prep kernel evaluates them once per (pass, state) — the
+// Pauli draws, the sub-gate products and the factored form (SiteMat in
+// dtc_kernels.hip) — instead of once per tile.  Per (pass, state):
+//   rec[k], rec[12 + k]  pre / post kick of tile bit k
+//       RX/RY family: d[0] = coefficient, i[1] = variant;  general: d[0..7] = 2x2
+//   rec[24]              d[0], d[1] = global factor (i^k * prod of scales),
+//                        d[2] = 1 / w_post^2 (measurement before the post-kick)
+union KickRec {
+  double d[8];
+  long long i[8];
+};
+static constexpr int kRecPerState = 2 * kTileBits + 1;
+static constexpr int kRecTotal = 2 * kTileBits;
+
+// One pass's kick layers, as the prep kernel needs them.
+struct PassKick {
+  KickDesc pre, post;   // enabled = 0: no such layer
+  int kind;             // KickKind of the pass
+  int c, s, act;        // tile geometry (see PassArgs)
+};
+
+struct PrepArgs {
+  const PassKick* passes;  // [n_pass] (device), or null: use `one`
+  PassKick one;
+  int n_pass;
+  int batch;
+  int64_t batch_start;
+  int n_traj;
+  int64_t traj_offset;
+  const double2* kick;     // [n_periods][L_kick][n_sub][4]
+  int n_sub;
+  int L_kick;              // sites per kick-table row (logical chain length)
+  int L_real;              // physical sites of the state
+  const int* site_of;      // physical index bit -> logical site (sharded states); null = identity
+  uint32_t thr1, thr2, thr3;
+  uint64_t seed;
+  int noisy;
+  KickRec* out;            // [n_pass][batch][kRecPerState]
+};
+
 // One streaming pass over a batch of states.  A tile covers index bits
 // [0, c) ∪ [s, s + 12 - c); tile bit k < c is global bit k, tile bit k >= c is
 // global bit s + k - c.  The pass applies, in order:
@@ -64,21 +105,11 @@ struct PassArgs {
   int c, s;                // tile geometry
   int tile_bits_mid;       // s - c  (tile-id bits deposited at [c, s))
   int act;                 // active tile-bit mask (sites kicked by this pass)
-  // batch -> (instance, trajectory)
+  // batch -> instance: inst = (batch_start + b) / n_traj
   int batch;               // states in this launch
   int64_t batch_start;
   int n_traj;
-  int64_t traj_offset;
-  // kicks
-  const double2* kick;     // [n_periods][L_kick][n_sub][4]
-  int n_sub;
-  int L_kick;              // sites per kick-table row (logical chain length)
-  const int* site_of;      // physical index bit -> logical site (sharded states); null = identity
-  KickDesc pre, post;
-  // noise
-  uint32_t thr1, thr2, thr3;
-  uint64_t seed;
-  int noisy;
+  const KickRec* recs;     // [batch][kRecPerState] of this pass (prep kernel)
   // diagonal factor tables, per instance: n_chunks chunk tables then one
   // 64-entry window table per start bit g0 = 0 .. L_eff-1
   const double2* diag;
@@ -93,6 +124,9 @@ struct PassArgs {
   double* partial;         // [B][n_tiles][n_obs]
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
+
+// Kick records of n_pass passes x batch states.
+hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
 
 // act must cover nibble sets {2}, {1,2} or {0,1,2}; L_eff in [12, 32].
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);

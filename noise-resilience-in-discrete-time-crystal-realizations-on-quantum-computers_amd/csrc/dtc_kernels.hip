@@ -85,21 +85,9 @@ __device__ __forceinline__ void dagger(double2* m) {
   m[2] = make_double2(m01.x, -m01.y);
 }
 
-// Noisy kick of one site for one layer (see KickMode), in two steps so the
-// gate-table loads can be issued before a tile's amplitude loads (vector
-// memory returns in order: a load issued after the tile would make the
-// setup wait for the whole tile).
-static constexpr int kPreSub = 2;  // sub-gates whose tables are loaded up front
-
-__device__ __forceinline__ const double2* kick_gate_ptr(const PassArgs& A, const KickDesc& K,
-                                                        int site, int q) {
-  const int qq = (K.mode == kKickInverse) ? (A.n_sub - 1 - q) : q;
-  return A.kick + (((int64_t)K.row * A.L_kick + site) * A.n_sub + qq) * 4;
-}
-
-__device__ __forceinline__ void build_site_kick(const PassArgs& A, const KickDesc& K, int site,
-                                                uint64_t traj, const double2 (&pre)[kPreSub][4],
-                                                double2* m) {
+// Noisy kick of one site for one layer (see KickMode).
+__device__ void build_site_kick(const PrepArgs& P, const KickDesc& K, int site, uint64_t traj,
+                                double2* m) {
   m[0] = make_double2(1.0, 0.0);
   m[1] = make_double2(0.0, 0.0);
   m[2] = make_double2(0.0, 0.0);
@@ -111,28 +99,16 @@ __device__ __forceinline__ void build_site_kick(const PassArgs& A, const KickDes
     m[2] = make_double2(r, 0.0); m[3] = make_double2(-r, 0.0);
     return;
   }
-  auto apply = [&](int q, double2* gm) {
+  for (int q = 0; q < P.n_sub; ++q) {
+    const int qq = inv ? (P.n_sub - 1 - q) : q;
+    const double2* gp = P.kick + (((int64_t)K.row * P.L_kick + site) * P.n_sub + qq) * 4;
+    double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
     if (inv) dagger(gm);
     mat_mul(m, gm, m);
-    if (A.noisy) {
-      int p = sample_pauli(A.seed, traj, K.stream, K.rng_period, (uint32_t)site, (uint32_t)q,
-                           A.thr1, A.thr2, A.thr3);
+    if (P.noisy) {
+      int p = sample_pauli(P.seed, traj, K.stream, K.rng_period, (uint32_t)site, (uint32_t)q,
+                           P.thr1, P.thr2, P.thr3);
       pauli_left(m, p);
-    }
-  };
-  if (A.n_sub <= kPreSub) {
-#pragma unroll
-    for (int q = 0; q < kPreSub; ++q) {  // static register indices: no scratch
-      if (q < A.n_sub) {
-        double2 gm[4] = {pre[q][0], pre[q][1], pre[q][2], pre[q][3]};
-        apply(q, gm);
-      }
-    }
-  } else {  // > kPreSub sub-gates per site (generic circuits): reload from the table
-    for (int q = 0; q < A.n_sub; ++q) {
-      const double2* gp = kick_gate_ptr(A, K, site, q);
-      double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
-      apply(q, gm);
     }
   }
   if (K.mode == kKickUndo || K.mode == kKickUndoBasisX) dagger(m);
@@ -200,6 +176,66 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
   sm.var = (form_b ? 2 : 0) | (neg ? 1 : 0);
 }
 
+// Kick records (dtc_kernels.h: KickRec) of n_pass passes x batch states: one
+// thread per (pass, state) builds the 24 noisy site kicks of the pass, writes
+// their factored forms and the product of their global factors.
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (int64_t)P.n_pass * P.batch) return;
+  const int pass = (int)(id / P.batch);
+  const int b = (int)(id % P.batch);
+  const PassKick pk = P.passes ? P.passes[pass] : P.one;
+  const int64_t gstate = P.batch_start + b;
+  const uint64_t traj = (uint64_t)(P.traj_offset + (gstate % P.n_traj));
+  KickRec* out = P.out + id * kRecPerState;
+  int ksum = 0;
+  double w[2] = {1.0, 1.0};
+  for (int half = 0; half < 2; ++half) {
+    const KickDesc& K = half == 0 ? pk.pre : pk.post;
+    for (int k = 0; k < kTileBits; ++k) {
+      const int lsite = k < pk.c ? k : pk.s + k - pk.c;
+      double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0),
+                      make_double2(1.0, 0.0)};
+      if (K.enabled && (pk.act & ~(int)K.skip & (1 << k)) && lsite < P.L_real) {
+        const int site = P.site_of ? P.site_of[lsite] : lsite;
+        build_site_kick(P, K, site, traj, m);
+      }
+      SiteMat sm;
+      canonicalise(pk.kind, m, sm);
+      KickRec r;
+      if (pk.kind == kKindGen) {
+        for (int e = 0; e < 4; ++e) {
+          r.d[2 * e] = sm.m[e].x;
+          r.d[2 * e + 1] = sm.m[e].y;
+        }
+      } else {
+        r.d[0] = sm.coef;
+        r.i[1] = sm.var;
+        for (int e = 2; e < 8; ++e) r.d[e] = 0.0;
+      }
+      out[half * kTileBits + k] = r;
+      ksum += sm.k;
+      w[half] *= sm.scale;
+    }
+  }
+  const int kph = ksum & 3;
+  const double wg = w[0] * w[1];
+  KickRec tot;
+  for (int e = 0; e < 8; ++e) tot.d[e] = 0.0;
+  tot.d[0] = kph == 0 ? wg : (kph == 2 ? -wg : 0.0);
+  tot.d[1] = kph == 1 ? wg : (kph == 3 ? -wg : 0.0);
+  tot.d[2] = 1.0 / (w[1] * w[1]);
+  out[kRecTotal] = tot;
+}
+
+hipError_t launch_prep(const PrepArgs& a, hipStream_t stream) {
+  if (!a.passes && a.n_pass != 1) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)a.n_pass * a.batch;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
 // Tile layouts: register r of lane-thread t holds tile index Y(t, r) =
 // ybase<LAY>(t) | (r << 4 LAY).
 // Layout 2: registers = tile bits 8..11, threads = bits 0..7 (coalesced).
@@ -218,15 +254,6 @@ __device__ __forceinline__ int tile_y(int t, int r) {
 // XOR swizzle over 16-B slots: conflict-free ds_write_b128 / ds_read_b128 for
 // every layout transition used here (MI355X_MICROARCH.md §LDS lane groups).
 __device__ __forceinline__ int lds_slot(int y) { return y ^ ((y >> 4) & 15); }
-
-// Wave-uniform copy of an LDS value (the matrices are identical across the
-// workgroup): SGPR coefficients, no per-lane copies.
-__device__ __forceinline__ double uni(double x) {
-  const long long v = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 // Factored RX-family butterfly (see SiteMat): (u, v) <- diag(1, sigma) S (u, v)
 template <int VAR>
@@ -280,41 +307,53 @@ __device__ __forceinline__ void layer_f(double2 (&v)[kRegs], double f) {
   }
 }
 
+// The kick records of a (pass, state) — 25 x 64 B — live in the VGPRs of
+// every wave: lane l holds doubles [4l, 4l + 4) of the block (loaded with the
+// setup, before the tile); a coefficient is two v_readlane_b32 with static
+// lane and register indices: no LDS, no scalar-memory round trip per layer.
+struct RecRegs {
+  double rv[4];
+  __device__ __forceinline__ long long bits(int j) const {
+    const long long x = __double_as_longlong(rv[j & 3]);
+    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), j >> 2);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), j >> 2);
+    return ((long long)hi << 32) | (unsigned int)lo;
+  }
+  __device__ __forceinline__ double d(int rec, int e) const {
+    return __longlong_as_double(bits(8 * rec + e));
+  }
+  __device__ __forceinline__ int i(int rec, int e) const { return (int)bits(8 * rec + e); }
+};
+
 template <int N, int KIND>
-__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const SiteMat* s_mat, int act) {
+__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs& R, int rec0) {
   // Every site of an active nibble runs (inactive sites carry the identity):
   // no data-dependent branches, so no register shuffles at merge points; the
   // RX/RY variant branch is wave-uniform.
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int k = 4 * N + q;
-    {
-      // keep the scheduler from hoisting every layer's coefficient loads to
-      // the top of the pass (register pressure -> spills)
-      __builtin_amdgcn_sched_barrier(0);
-      if (KIND == kKindGen) {
-        double2 m[4];
+    const int k = rec0 + 4 * N + q;
+    if (KIND == kKindGen) {
+      double2 m[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          m[e] = make_double2(uni(s_mat[k].m[e].x), uni(s_mat[k].m[e].y));
+      for (int e = 0; e < 4; ++e) m[e] = make_double2(R.d(k, 2 * e), R.d(k, 2 * e + 1));
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r)
-          if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
-      } else {
-        const double f = uni(s_mat[k].coef);
-        const int var = __builtin_amdgcn_readfirstlane(s_mat[k].var);
-        auto run = [&](auto qtag) {
-          constexpr int Q = decltype(qtag)::value;
-          if (var == 0) layer_f<KIND, 0, Q>(v, f);
-          else if (var == 1) layer_f<KIND, 1, Q>(v, f);
-          else if (var == 2) layer_f<KIND, 2, Q>(v, f);
-          else layer_f<KIND, 3, Q>(v, f);
-        };
-        if (q == 0) run(std::integral_constant<int, 0>{});
-        else if (q == 1) run(std::integral_constant<int, 1>{});
-        else if (q == 2) run(std::integral_constant<int, 2>{});
-        else run(std::integral_constant<int, 3>{});
-      }
+      for (int r = 0; r < kRegs; ++r)
+        if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
+    } else {
+      const double f = R.d(k, 0);
+      const int var = R.i(k, 1);
+      auto run = [&](auto qtag) {
+        constexpr int Q = decltype(qtag)::value;
+        if (var == 0) layer_f<KIND, 0, Q>(v, f);
+        else if (var == 1) layer_f<KIND, 1, Q>(v, f);
+        else if (var == 2) layer_f<KIND, 2, Q>(v, f);
+        else layer_f<KIND, 3, Q>(v, f);
+      };
+      if (q == 0) run(std::integral_constant<int, 0>{});
+      else if (q == 1) run(std::integral_constant<int, 1>{});
+      else if (q == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
     }
   }
 }
@@ -390,22 +429,27 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double2 s_tile[kTile];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
-  __shared__ SiteMat s_pre[RP::pre ? kTileBits : 1];
-  __shared__ SiteMat s_post[RP::post ? kTileBits : 1];
-  __shared__ int s_kc[2];
-  __shared__ double s_w[2];
   __shared__ double s_red[kThreads / 64][kMaxObs];
 
   const int t = threadIdx.x;
-  const int act = A.act;
   const int c = A.c, s = A.s;
   const int tile_bits = A.L_eff - kTileBits;
   const int64_t n_tiles = (int64_t)1 << tile_bits;
   const int64_t b = blockIdx.y;
   const int64_t tile = blockIdx.x;
-  const int64_t gstate = A.batch_start + b;
-  const int inst = (int)(gstate / A.n_traj);
-  const uint64_t traj = (uint64_t)(A.traj_offset + (gstate % A.n_traj));
+  const int inst = (int)((A.batch_start + b) / A.n_traj);
+  // this state's kick records (prep kernel), lane-distributed (RecRegs)
+  RecRegs R;
+  {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < 8 * kRecPerState) {
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
 
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
@@ -414,32 +458,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   M.cmask = (1 << c) - 1;
   M.tbase = ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
 
-  // ---- phase 1: the setup's global loads (kick gates of this thread's site,
-  // diagonal tables of the state's instance), issued before the tile ----
-  const bool is_pre = RP::pre && t < kTileBits;
-  const bool is_post = RP::post && t >= 64 && t < 64 + kTileBits;
-  const int k = is_pre ? t : t - 64;
-  const KickDesc& K = is_pre ? A.pre : A.post;
-  int site = 0;
-  bool kick_on = false;
-  double2 gpre[kPreSub][4];
-  if (is_pre || is_post) {
-    const int lsite = k < c ? k : s + k - c;
-    kick_on = (act & ~(int)K.skip & (1 << k)) && lsite < A.L_real;
-    if (kick_on) {
-      site = A.site_of ? A.site_of[lsite] : lsite;  // sharded: physical bit -> logical site
-      if (K.mode != kKickBasisX) {
-#pragma unroll
-        for (int q = 0; q < kPreSub; ++q) {
-          if (q < A.n_sub) {
-            const double2* gp = kick_gate_ptr(A, K, site, q);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) gpre[q][e] = gp[e];
-          }
-        }
-      }
-    }
-  }
+  // ---- diagonal tables of the state's instance: loads issued before the
+  // tile's (vector memory returns in order), staged to LDS below ----
   constexpr int kChunkPerThread = (kMaxChunks * 64 + kThreads - 1) / kThreads;
   double2 dchunk[kChunkPerThread];
   double2 dwin = make_double2(1.0, 0.0);
@@ -456,8 +476,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     if (g0 >= 0 && t < 64) dwin = dt[(A.n_chunks + g0) * 64 + t];
   }
 
-  // ---- phase 2: the tile (coalesced 16-B loads: uniform 64-bit base +
-  // one per-lane 32-bit byte offset shared by all 16 accesses, L_eff <= 32) ----
+  // ---- the tile (coalesced 16-B loads: uniform 64-bit base + one per-lane
+  // 32-bit byte offset shared by all 16 accesses, L_eff <= 32) ----
   const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
   double2 v[kRegs];
   {
@@ -466,62 +486,30 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int r = 0; r < kRegs; ++r)
       v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
   }
+  DTC_TS(1);
   // vmcnt(16) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt/lgkmcnt
-  // unmasked): the setup loads have landed, the tile's 16 are still in flight.
-  // Explicit, so the divergent setup code below never waits for the tile.
+  // unmasked): the record and table loads have landed, the tile's 16 are in
+  // flight.  Explicit, so no use of them waits for the tile.
   static_assert(kRegs == 16, "vmcnt immediate assumes 16 tile loads");
   __builtin_amdgcn_s_waitcnt(0x4F70);
-  DTC_TS(1);
-
-  // ---- phase 3: setup compute while the tile is in flight: noisy kick
-  // matrices (threads 0..11 pre, 64..75 post), their global phase, tables ----
-  {
-    int kk = 0;
-    double wscale = 1.0;
-    if (is_pre || is_post) {
-      double2 m[4];
-      if (kick_on) {
-        build_site_kick(A, K, site, traj, gpre, m);
-      } else {  // inactive tile bits and padding sites: identity
-        m[0] = make_double2(1.0, 0.0); m[1] = make_double2(0.0, 0.0);
-        m[2] = make_double2(0.0, 0.0); m[3] = make_double2(1.0, 0.0);
-      }
-      SiteMat sm;
-      canonicalise(KIND, m, sm);
-      if (is_pre) s_pre[k] = sm;
-      else s_post[k] = sm;
-      kk = sm.k;
-      wscale = sm.scale;
-    }
-    // i^k phases: k is 0 or 1 per site; waves 0 (pre) and 1 (post) count them
-    // and multiply the sites' real scales w
-    const unsigned long long bal = __ballot(kk != 0);
-    double w = wscale;
+  if (RP::diag) {
+    const double cs = A.diag_conj ? -1.0 : 1.0;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) w *= __shfl_xor(w, off, 64);
-    if (t == 0) { s_kc[0] = __popcll(bal); s_w[0] = w; }
-    if (t == 64) { s_kc[1] = __popcll(bal); s_w[1] = w; }
-    if (RP::diag) {
-      const double cs = A.diag_conj ? -1.0 : 1.0;
-#pragma unroll
-      for (int j = 0; j < kChunkPerThread; ++j) {
-        const int i = t + j * kThreads;
-        if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
-      }
-      if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    for (int j = 0; j < kChunkPerThread; ++j) {
+      const int i = t + j * kThreads;
+      if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
     }
+    if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    // made visible by the first exchange's barrier, or by this one
+    if constexpr (!(RP::pre && (RP::n0 || RP::n1))) __syncthreads();
   }
-  __syncthreads();  // matrices, phases and tables ready
   DTC_TS(2);
-  const int kph = __builtin_amdgcn_readfirstlane(s_kc[0] + s_kc[1]) & 3;
   // global factor of the factored kicks, i^k * w_pre * w_post, applied with
   // the diagonal (the state's arithmetic does not depend on whether it is
   // measured; a measurement between the diagonal and the post-kick divides
   // its sums by w_post^2)
-  const double w_post = RP::post ? s_w[1] : 1.0;
-  const double wg = (RP::pre ? s_w[0] : 1.0) * w_post;
-  const double2 gph = make_double2(kph == 0 ? wg : (kph == 2 ? -wg : 0.0),
-                                   kph == 1 ? wg : (kph == 3 ? -wg : 0.0));
+  const double2 gph = make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1));
+  const double inv_w2_mid = R.d(kRecTotal, 2);
 
   auto diag_in = [&](auto lay_tag) {
     constexpr int LAY = decltype(lay_tag)::value;
@@ -615,14 +603,14 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
   if constexpr (RP::pre) {
-    if constexpr (RP::n2) apply_nibble<2, KIND>(v, s_pre, act);
+    if constexpr (RP::n2) apply_nibble<2, KIND>(v, R, 0);
     if constexpr (RP::n0) {
       exchange<2, 0>(v, s_tile, t);
-      apply_nibble<0, KIND>(v, s_pre, act);
+      apply_nibble<0, KIND>(v, R, 0);
     }
     if constexpr (RP::n1) {
       exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
-      apply_nibble<1, KIND>(v, s_pre, act);
+      apply_nibble<1, KIND>(v, R, 0);
     }
   }
   DTC_TS(3);
@@ -635,21 +623,21 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // ---- diagonal and measurement at d_lay ----
   using DL = std::integral_constant<int, RP::d_lay>;
   if constexpr (RP::diag) diag_in(DL{});
-  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{}, 1.0 / (w_post * w_post));  // before the post-kick
+  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{}, inv_w2_mid);  // before the post-kick
   DTC_TS(4);
   // ---- post-kick rounds: 1 -> 0 -> 2 ----
   if constexpr (RP::post) {
     if constexpr (RP::n1) {
       exchange<RP::d_lay, 1>(v, s_tile, t);
-      apply_nibble<1, KIND>(v, s_post, act);
+      apply_nibble<1, KIND>(v, R, kTileBits);
     }
     if constexpr (RP::n0) {
       exchange<RP::p1, 0>(v, s_tile, t);
-      apply_nibble<0, KIND>(v, s_post, act);
+      apply_nibble<0, KIND>(v, R, kTileBits);
     }
     if constexpr (RP::n2) {
       exchange<RP::p0, 2>(v, s_tile, t);
-      apply_nibble<2, KIND>(v, s_post, act);
+      apply_nibble<2, KIND>(v, R, kTileBits);
     }
     exchange<RP::p2, 2>(v, s_tile, t);
   } else {
