@@ -358,10 +358,12 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs&
   }
 }
 
+// Tile re-layout through LDS.  No barrier before the writes: a thread writes
+// exactly the slots it read itself in the previous exchange (that one ended in
+// layout FROM), so no other thread can still need them.
 template <int FROM, int TO>
 __device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, int t) {
   if (FROM == TO) return;
-  __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y<FROM>(t, r))] = v[r];
   __syncthreads();
@@ -424,6 +426,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
 #ifdef DTC_PHASE_TIMING
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
   DTC_TS(0);
   __shared__ double2 s_tile[kTile];
@@ -653,9 +656,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
 #ifdef DTC_PHASE_TIMING
   DTC_TS(6);
   if (A.dbg_ts && t < 8 && SHAPE == DTC_PHASE_TIMING) {
-    // t 0..6: phase stamps (s_memtime); 7: HW_ID (CU/SIMD/XCC placement)
-    const uint64_t val = t < 7 ? ts[t & 7] : (uint64_t)__builtin_amdgcn_s_getreg(
-                                                 (4 << 0) | (0 << 6) | (31 << 11));
+    // t 0..6: phase stamps (s_memtime, per-XCD clock); 7: s_memrealtime
+    // (100 MHz, chip-wide) start in bits 0..31, duration in bits 32..59
+    const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
+    const uint64_t val = t < 7 ? ts[t & 7]
+                               : ((rt_start & 0xffffffffull) | ((rt_end - rt_start) << 32));
     A.dbg_ts[(b * n_tiles + tile) * 8 + t] = val | ((uint64_t)NIBS << 60);
   }
 #endif

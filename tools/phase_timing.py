@@ -39,16 +39,16 @@ for nb in sorted(set(nibs.tolist())):
     sel = a[nibs == nb]
     if nb == 0 or len(sel) == 0:
         continue
-    t0 = sel[:, 0].min()
-    span = sel[:, 6].max() - t0
+    rt0 = sel[:, 7] & 0xffffffff
+    rtd = (sel[:, 7] >> 32) & ((1 << 28) - 1)
+    span = (rt0 + rtd).max() - rt0.min()   # 10 ns ticks
+    life = sel[:, 6] - sel[:, 0]
+    print(f"NIBS={nb}: {len(sel)} workgroups, launch span {span * 10 / 1000:.1f} us, "
+          f"median lifetime {np.median(life):.0f} clk = {np.median(rtd) * 10 / 1000:.2f} us, "
+          f"mean concurrency {rtd.sum() / span:.0f} workgroups")
     d = np.diff(sel[:, :7], axis=1)
     life = sel[:, 6] - sel[:, 0]
     names = ["issue+setup-loads", "setup(barrier)", "pre-rounds", "diag", "post-rounds", "store"]
-    print(f"NIBS={nb}: {len(sel)} workgroups, launch span {span} clk, "
-          f"median lifetime {np.median(life):.0f} clk, sum of lifetimes / span = "
-          f"{life.sum() / span:.1f} concurrent")
     for i, n in enumerate(names):
         print(f"   {n:20s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f}  "
               f"p90 {np.percentile(d[:, i], 90):8.0f}")
-    hw = sel[:, 7]
-    print("   distinct HW_ID:", len(set(hw.tolist())))
