@@ -110,8 +110,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-traj", type=int, default=0, help="0 = one per host thread")
     ap.add_argument("--cpu-tf", type=int, default=8)
-    ap.add_argument("--config", choices=("c2", "c4", "c5"), default="c2",
-                    help="c2: BASELINE configs[1] (default, the headline line); c4: L=28 "
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2",
+                    help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
+                         "device-like noise (stand-in calibration, data/"
+                         "device_standin_L20.json), 1024 trajectories per step; c4: L=28 "
                          "noiseless disorder sweep, instances sharded over ranks; c5: one "
                          "L=34 state sharded over the ranks (1 GPU: --L 31, 8 virtual ranks)")
     ap.add_argument("--shard-bits", type=int, default=3, help="c5: log2 of the shard count")
@@ -141,6 +143,13 @@ def main():
     hs, phis = load_disorder_row(args.L)
     spec = pkg.SweepSpec(L=args.L, T=args.tf, hs=hs, phis=phis, g=0.97, noise_prob=0.05,
                          use_noise=1, initial_state="vacuum")
+    c3 = args.config == "c3"
+    if c3:  # device-like noise, throughput only (parity unpinned)
+        cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data",
+                                                           "device_standin_L20.json"))
+        spec.device = cal.device_noise(args.L)
+        if args.batch == 256:
+            args.batch = 1024
     eng = pkg.DtcEngine(local_rank)
     B = args.batch
     T = args.tf
@@ -197,14 +206,14 @@ def main():
     traffic, traffic_src = read_traffic(launch_bytes)
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not c3:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         ntr = args.cpu_traj or threads
         cpu = cpu_baseline(spec, ntr, args.cpu_tf, threads)
 
     info = eng.device_info()
     res = {
-        "metric": METRIC,
+        "metric": METRIC if not c3 else METRIC.replace("at L=20", "at L=20 (C3 device-like noise)"),
         "value": value,
         "unit": "periods*instances/s",
         "n_gpus": world,
@@ -217,8 +226,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": (f"DTC autocorrelator sweep, L={args.L}, g=0.97, tf={T}, depolarizing "
-                         f"p=0.05, 1 disorder instance (hs/phis_L{args.L}.csv row 0), "
+            "workload": (f"DTC autocorrelator sweep, L={args.L}, g=0.97, tf={T}, "
+                         + ("device-like noise (T1/T2 relaxation + depolarizing + read-out, "
+                            "stand-in calibration data/device_standin_L20.json)" if c3 else
+                            "depolarizing p=0.05")
+                         + f", 1 disorder instance (hs/phis_L{args.L}.csv row 0), "
                          f"{B} noisy trajectories per step per GPU, forward+echo"),
             "L": args.L, "tf": T, "g": 0.97, "noise_prob": 0.05,
             "trajectories_per_step_per_gpu": B,

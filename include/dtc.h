@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 2
+#define DTC_ABI_VERSION 3
 
 /* error codes */
 #define DTC_OK 0
@@ -89,6 +89,30 @@ typedef struct dtc_noise {
   int32_t reserved;
 } dtc_noise;
 
+/* Device-like noise (the reference's
+ * use_fakebackend=1 path, NoiseModel.from_backend(FakeBrisbane()) at
+ * fast.py:77-79, whose calibration data is not available offline: the caller
+ * supplies per-site calibration).  After every kick sub-gate on site i:
+ *   thermal relaxation  amplitude damping gamma_i = 1 - exp(-gate_ns / T1_i)
+ *                       and pure dephasing to the total coherence decay
+ *                       exp(-gate_ns / T2_i)  (T2 clamped to 2 T1),
+ *   then depolarizing_error(p_gate_i, 1).
+ * Trajectories stay linear: the amplitude-damping Kraus operator is drawn with
+ * fixed probabilities (jump w.p. gamma/2) and weighted by 1/sqrt(prob), so the
+ * trajectory mean of the (unnormalized) <Z_j> is the exact channel's.  The
+ * neel-prep X gates get the Pauli part only.  The ancilla enters as
+ *   a = anc_factor * z_j(init) * <Z_j>,  reported as the read-out value
+ *   (1 - p01 - p10) a + (p10 - p01)   (P(read 1|0) = p01, P(read 0|1) = p10). */
+typedef struct dtc_device_noise {
+  const double* p_gate;  /* [L] depolarizing parameter per kick sub-gate   */
+  const double* t1_us;   /* [L] T1 (microseconds; <= 0 or inf: none)      */
+  const double* t2_us;   /* [L] T2 (microseconds; <= 0 or inf: none)      */
+  double gate_ns;        /* duration of one kick sub-gate                  */
+  double anc_factor;     /* ancilla coherence factor ((1-p)^6 in fast.py)  */
+  double readout_p01;    /* ancilla read-out P(1 | 0)                      */
+  double readout_p10;    /* ancilla read-out P(0 | 1)                      */
+} dtc_device_noise;
+
 /* Context management. device = HIP device ordinal. */
 int dtc_open(int32_t device, dtc_ctx** out);
 int dtc_close(dtc_ctx* ctx);
@@ -107,6 +131,13 @@ int32_t dtc_abi_version(void);
 int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
                  uint64_t seed, int64_t traj_offset, int32_t n_traj,
                  double* fwd, double* echo, double* zsite);
+
+/* dtc_autocorr under device-like noise (dtc_device_noise above); noise->p
+ * and noise->n_anc are ignored.  Outputs as dtc_autocorr (zsite: unnormalized
+ * per-site <Z_i>, nullable). */
+int dtc_autocorr_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_noise* dev,
+                        uint64_t seed, int64_t traj_offset, int32_t n_traj, double* fwd,
+                        double* echo, double* zsite);
 
 /* Unit-test hook: apply n_periods Floquet periods to one host state vector
  * of 2^L complex128 amplitudes (in/out).  Forward: periods first_period,

@@ -22,6 +22,8 @@ from . import circuit, aer, sweep, distributed, sharded, energy, envelopes, cont
 from . import cli, energy_cli, control_cli  # noqa: E402
 from .circuit import QuantumCircuit, transpile_aer_basis  # noqa: E402
 from .aer import AerSimulator, DtcSimulator, NoiseModel, depolarizing_error  # noqa: E402
+from .device_noise import DeviceNoise, DeviceCalibration  # noqa: E402
+from . import device_noise  # noqa: E402
 from .sweep import (run_sweep, get_instances, get_single_out,  # noqa: E402
                     compute_z_expectation, write_autocorr_csv)
 
@@ -32,5 +34,5 @@ __all__ = [
     "DtcSimulator", "NoiseModel", "depolarizing_error", "run_sweep", "get_instances",
     "get_single_out", "compute_z_expectation", "write_autocorr_csv", "circuit", "aer",
     "sweep", "distributed", "sharded", "energy", "envelopes", "control", "cli", "energy_cli",
-    "control_cli",
+    "control_cli", "DeviceNoise", "DeviceCalibration", "device_noise",
 ]

@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "dtc_shard_step",
     "dtc_plan_groups",
     "dtc_energy",
+    "dtc_autocorr_device",
 )
 
 KERNEL_LO_PASS = 0
@@ -75,6 +76,20 @@ class DtcNoise(ctypes.Structure):
         ("p", ctypes.c_double),
         ("n_anc", ctypes.c_int32),
         ("reserved", ctypes.c_int32),
+    ]
+
+
+class DtcDeviceNoise(ctypes.Structure):
+    """Mirror of ``dtc_device_noise`` (include/dtc.h)."""
+
+    _fields_ = [
+        ("p_gate", _dp),
+        ("t1_us", _dp),
+        ("t2_us", _dp),
+        ("gate_ns", ctypes.c_double),
+        ("anc_factor", ctypes.c_double),
+        ("readout_p01", ctypes.c_double),
+        ("readout_p10", ctypes.c_double),
     ]
 
 
@@ -146,6 +161,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_int32, _dp, _dp, _dp,
         ]
+        lib.dtc_autocorr_device.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcDeviceNoise), ctypes.c_uint64, ctypes.c_int64,
+            ctypes.c_int32, _dp, _dp, _dp,
+        ]
         lib.dtc_plan_groups.argtypes = [ctypes.c_int32, P(ctypes.c_uint64), ctypes.c_int32]
         for name in EXPORTED_SYMBOLS:
             if name not in ("dtc_last_error", "dtc_abi_version"):
@@ -165,6 +184,19 @@ def as_dptr(a: np.ndarray | None):
         return None
     assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(_dp)
+
+
+def device_struct(dev) -> "DtcDeviceNoise":
+    """dtc_device_noise view of a DeviceNoise (arrays stay owned by ``dev``)."""
+    d = DtcDeviceNoise()
+    d.p_gate = as_dptr(dev.p_gate)
+    d.t1_us = as_dptr(dev.t1_us)
+    d.t2_us = as_dptr(dev.t2_us)
+    d.gate_ns = float(dev.gate_ns)
+    d.anc_factor = float(dev.anc_factor)
+    d.readout_p01 = float(dev.readout_p01)
+    d.readout_p10 = float(dev.readout_p10)
+    return d
 
 
 def plan_groups(n_bits: int) -> list:

@@ -65,9 +65,19 @@ class NoiseModel:
 
     @classmethod
     def from_backend(cls, backend, **kw):
-        raise NotImplementedError(
-            "device noise (FakeBrisbane calibration, fast.py:77-79) is not available offline; "
-            "see DESIGN.md §Out of scope")
+        """fast.py:77-79.  FakeBrisbane's calibration ships inside
+        qiskit_ibm_runtime (not available offline); a ``FakeDevice`` built
+        from a calibration file gives the device-like noise path instead."""
+        if not isinstance(backend, FakeDevice):
+            raise NotImplementedError(
+                "NoiseModel.from_backend needs calibration data: FakeBrisbane's is not "
+                "available offline; use FakeDevice(<calibration.json>) "
+                "(data/device_standin_L20.json is a documented stand-in)")
+        nm = cls(basis_gates=["ecr", "id", "rz", "sx", "x"])
+        nm.device_calibration = backend.calibration
+        return nm
+
+    device_calibration = None
 
     @property
     def noise_instructions(self):
@@ -78,7 +88,19 @@ class NoiseModel:
         return self._errors.get(carrier) if carrier else None
 
     def is_ideal(self):
-        return not self._errors
+        return not self._errors and self.device_calibration is None
+
+
+class FakeDevice:
+    """A backend-like calibration holder for NoiseModel.from_backend (the
+    stand-in for fast.py's FakeBrisbane(), device_noise.py)."""
+
+    def __init__(self, calibration_path: str):
+        from .device_noise import DeviceCalibration
+
+        self.calibration = DeviceCalibration.from_json(calibration_path)
+        self.name = self.calibration.name
+        self.num_qubits = len(self.calibration.qubits)
 
 
 @dataclass
@@ -328,10 +350,23 @@ class DtcSimulator:
         seed = seed_simulator if seed_simulator is not None else self.seed_simulator
         if seed is None:
             seed = int(np.random.SeedSequence().generate_state(1, np.uint64)[0])
-        p = _noise_p(self.noise_model)
+        cal = getattr(self.noise_model, "device_calibration", None)
+        p = 0.0 if cal is not None else _noise_p(self.noise_model)
         eng = get_engine(self.device_index)
         counts, expv = [], []
         for ci, circ in enumerate(circs):
+            if cal is not None:
+                a = _run_device(eng, circ, cal, shots, seed + 7919 * (self._calls + ci))
+                rng = np.random.default_rng([seed, self._calls, ci])
+                n0 = int(rng.binomial(shots, float(np.clip((1.0 + a) / 2.0, 0.0, 1.0))))
+                c = {}
+                if n0:
+                    c["0"] = n0
+                if shots - n0:
+                    c["1"] = shots - n0
+                counts.append(c)
+                expv.append(a)
+                continue
             f = fold_circuit(circ, self.noise_model)
             # kicks and X preps both transpile to u3: one noise probability for both
             pk = p if (f.kick_noisy or f.prep_noisy) else 0.0
@@ -377,6 +412,20 @@ def _run_single(eng: DtcEngine, spec: SweepSpec, f: FoldedCircuit, n_traj: int, 
         _capi.as_dptr(echo if f.echo else None), None))
     a = (echo if f.echo else fwd)[0, :, T - 1]
     return a * (1.0 - p_anc) ** f.n_anc_noisy
+
+
+def _run_device(eng: DtcEngine, circ, cal, shots: int, seed: int) -> float:
+    """Trajectory-mean read-out expectation of one folded circuit under the
+    calibration's device-like noise (dtc_autocorr_device)."""
+    f = fold_circuit(circ, None)
+    T = f.n_fwd + 1
+    dev = cal.device_noise(f.L)  # every kick is a physical (noisy) gate on the device
+    spec = SweepSpec(L=f.L, T=T, hs=f.hs, phis=f.phis, kick=f.kick, probe_site=f.probe,
+                     init_mask_value=f.init_mask, device=dev)
+    out = eng.autocorr(spec, max(1, shots), seed=seed & (2**64 - 1),
+                       want_fwd=not f.echo, want_echo=f.echo, t_first=T - 1)
+    a = (out["echo"] if f.echo else out["fwd"])[0, :, T - 1]
+    return float(np.mean(a))
 
 
 AerSimulator = DtcSimulator

@@ -20,10 +20,16 @@ import time
 
 import numpy as np
 
+from .device_noise import DeviceCalibration
 from .disorder import load_disorder
 from .engine import SweepSpec
 from .kicks import POLARIZATIONS
 from . import sweep as sw
+
+# documented stand-in calibration (data/device_standin_L20.json): the reference's
+# FakeBrisbane snapshot is not available offline
+DEFAULT_CALIBRATION = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "data", "device_standin_L20.json")
 
 
 def build_parser():
@@ -40,7 +46,11 @@ def build_parser():
     p.add_argument("--use_noise", type=int, default=1, help="0=no noise, 1=apply noise")
     p.add_argument("--initial_state", type=str, default="vacuum", choices=["vacuum", "neel"])
     p.add_argument("--use_fakebackend", type=int, default=0,
-                   help="1 = FakeBrisbane noise (not available offline: error)")
+                   help="1 = device-like noise (thermal relaxation + depolarizing + read-out) "
+                        "from --device_calibration; FakeBrisbane's own data is not available "
+                        "offline")
+    p.add_argument("--device_calibration", type=str, default=DEFAULT_CALIBRATION,
+                   help="calibration JSON for --use_fakebackend 1 (device-like noise)")
     p.add_argument("--polarization", type=str, default="x", choices=list(POLARIZATIONS))
     p.add_argument("--circular_frequency", type=float, default=1.0)
     # engine options
@@ -60,21 +70,25 @@ def build_parser():
 
 def main(argv=None):
     args = build_parser().parse_args(argv)
-    if args.use_fakebackend:
-        raise SystemExit("--use_fakebackend 1 needs FakeBrisbane calibration data, which is not "
-                         "available offline (DESIGN.md, out of scope)")
     L, T = args.L, args.tf
+    device = None
+    if args.use_fakebackend:
+        # fast.py:77-79 uses FakeBrisbane's calibration (not available offline):
+        # a user-supplied calibration file drives the device-like noise path
+        cal = DeviceCalibration.from_json(args.device_calibration)
+        device = cal.device_noise(L)
+        print(f"Device-like noise from {args.device_calibration} ({cal.name})")
     hs, phis = load_disorder(L, args.inst, args.disorder_folder)
     spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=args.g, polarization=args.polarization,
                      circular_frequency=args.circular_frequency,
                      initial_state=args.initial_state, noise_prob=args.noise_prob,
-                     use_noise=args.use_noise, t_offset=args.t_offset)
+                     use_noise=args.use_noise, t_offset=args.t_offset, device=device)
     shots = args.shots or None
-    if spec.p == 0:
+    if spec.p == 0 and device is None:
         n_traj = 1
     else:
         n_traj = args.trajectories or (shots or 1024)
-    if shots and spec.p > 0 and n_traj != shots:
+    if shots and spec.p > 0 and device is None and n_traj != shots:
         raise SystemExit("--trajectories must equal --shots when emulating shots (use --shots 0 "
                          "for trajectory means)")
 

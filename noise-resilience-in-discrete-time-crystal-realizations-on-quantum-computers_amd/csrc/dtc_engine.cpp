@@ -77,6 +77,7 @@ struct dtc_ctx {
   hipStream_t stream = nullptr;
   DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
   DevBuf recs, recs1, pk;               // kick records (batch schedule / single pass), pass list
+  DevBuf dev_thr, dev_jump, dev_kraus;  // device-like noise tables (dtc_autocorr_device)
   std::vector<dtc::PassKick> pk_host;   // staged pass list (alive until the stream syncs)
   bool prof = false;
   int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
@@ -235,6 +236,13 @@ struct RunCfg {
   int noisy;
   uint32_t thr1, thr2, thr3;
   const int* site_of = nullptr;  // device: physical bit -> logical site (shards)
+  // device-like noise (dtc_autocorr_device): general non-unitary kicks, no
+  // forward pass runs ahead of a branch point (a jump cannot be undone)
+  bool device = false;
+  std::vector<uint32_t> dev_thr_host;  // [L][3] per-site Pauli thresholds (prep X)
+  const uint32_t* dev_thr = nullptr;   // device copies
+  const uint32_t* dev_jump = nullptr;
+  const double* dev_kraus = nullptr;
 };
 
 // ---- layer chains ---------------------------------------------------------
@@ -248,6 +256,7 @@ struct Chain {
   int diag = dtc::kDiagFwd;
   std::vector<int> kc;      // layers applied per group
   int nd = 0;               // diagonals applied
+  bool post_after_d = true; // a pass that applies D may start the next layer
   int n() const { return (int)X.size() - 1; }
   int n_d() const { return trailing_d ? n() + 1 : n(); }
   bool done() const {
@@ -277,7 +286,7 @@ PassSpec next_pass(Chain& ch) {
   if (level && ch.nd < ch.n_d()) {
     ps.diag = ch.diag;
     ps.d_index = ++ch.nd;
-    if (ch.kc[G] == ch.nd && ch.kc[G] <= n) ps.post = ch.X[ch.kc[G]++];
+    if (ch.post_after_d && ch.kc[G] == ch.nd && ch.kc[G] <= n) ps.post = ch.X[ch.kc[G]++];
   }
   return ps;
 }
@@ -316,6 +325,9 @@ dtc::PrepArgs prep_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int
   P.thr3 = rc.thr3;
   P.seed = rc.seed;
   P.noisy = rc.noisy;
+  P.dev_thr = rc.dev_thr;
+  P.dev_thr_jump = rc.dev_jump;
+  P.dev_kraus = rc.dev_kraus;
   return P;
 }
 
@@ -353,7 +365,11 @@ int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
   for (const KickDesc* k : {&ps.pre, &ps.post}) {
     if (!k->enabled) continue;
     const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
-    const int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
+    int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
+    // device-like noise: Kraus x Pauli x gate is not unitary, but stays in
+    // the RX / RY family: the unfactored butterflies
+    if (rc.device && rk == dtc::kKindRX) rk = dtc::kKindRXU;
+    if (rc.device && rk == dtc::kKindRY) rk = dtc::kKindRYU;
     kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
   }
   return kind;
@@ -565,8 +581,11 @@ uint64_t init_state_mask(const RunCfg& rc, uint64_t traj) {
   if (!rc.noisy) return m;
   for (int i = 0; i < rc.pl.L; ++i) {
     if (!((rc.prob->init_mask >> i) & 1ull)) continue;
-    int pz = dtc::sample_pauli(rc.seed, traj, dtc::kStreamPrep, 0u, (uint32_t)i, 0u, rc.thr1,
-                               rc.thr2, rc.thr3);
+    int jump = 0;
+    int pz = rc.device ? dtc::sample_device(rc.seed, traj, dtc::kStreamPrep, 0u, (uint32_t)i, 0u,
+                                            rc.dev_thr_host.data() + 3 * i, 0u, &jump)
+                       : dtc::sample_pauli(rc.seed, traj, dtc::kStreamPrep, 0u, (uint32_t)i, 0u,
+                                           rc.thr1, rc.thr2, rc.thr3);
     if (pz == 1 || pz == 2) m &= ~(1ull << i);
   }
   return m;
@@ -708,6 +727,9 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->recs);
   release(ctx->recs1);
   release(ctx->pk);
+  release(ctx->dev_thr);
+  release(ctx->dev_jump);
+  release(ctx->dev_kraus);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return DTC_OK;
@@ -753,9 +775,74 @@ int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,
   return DTC_OK;
 }
 
-int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,
-                 int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
-                 double* zsite) {
+}  // extern "C"
+
+namespace {
+
+// Host-side tables of dtc_device_noise (see include/dtc.h for the model).
+int setup_device_noise(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_noise* dv,
+                       RunCfg& rc) {
+  const int L = pr->L;
+  if (!dv->p_gate || !dv->t1_us || !dv->t2_us) return fail(DTC_EINVAL, "null device-noise arrays");
+  if (!(dv->gate_ns >= 0.0)) return fail(DTC_EINVAL, "gate_ns must be >= 0");
+  if (!(dv->readout_p01 >= 0.0 && dv->readout_p01 <= 1.0 && dv->readout_p10 >= 0.0 &&
+        dv->readout_p10 <= 1.0))
+    return fail(DTC_EINVAL, "read-out errors must be in [0, 1]");
+  auto u32 = [](double prob) -> uint32_t {
+    double v = std::floor(prob * 4294967296.0 + 0.5);
+    if (v >= 4294967295.0) v = 4294967295.0;
+    if (v < 0) v = 0;
+    return (uint32_t)v;
+  };
+  std::vector<uint32_t> jump(L);
+  std::vector<double> kraus((size_t)3 * L);
+  rc.dev_thr_host.assign((size_t)3 * L, 0u);
+  for (int i = 0; i < L; ++i) {
+    const double p = dv->p_gate[i];
+    if (!(p >= 0.0 && p <= 4.0 / 3.0)) return fail(DTC_EINVAL, "p_gate out of range");
+    const double t1 = dv->t1_us[i] > 0.0 ? dv->t1_us[i] * 1e3 : INFINITY;  // ns
+    double t2 = dv->t2_us[i] > 0.0 ? dv->t2_us[i] * 1e3 : INFINITY;
+    t2 = std::min(t2, 2.0 * t1);
+    const double tg = dv->gate_ns;
+    const double gamma = std::isinf(t1) ? 0.0 : 1.0 - std::exp(-tg / t1);
+    // coherence left by amplitude damping: exp(-tg/(2 T1)); the rest is pure
+    // dephasing: Z with probability (1 - r)/2, r = exp(-tg (1/T2 - 1/(2 T1)))
+    const double rate = (std::isinf(t2) ? 0.0 : 1.0 / t2) - (std::isinf(t1) ? 0.0 : 0.5 / t1);
+    const double pz_deph = 0.5 * (1.0 - std::exp(-tg * std::max(0.0, rate)));
+    // dephasing then depolarizing(p): X, Y w.p. p/4, Z w.p. (1-d) p/4 + d (1 - 3p/4)
+    const double px = p / 4.0, py = p / 4.0;
+    const double pzz = (1.0 - pz_deph) * p / 4.0 + pz_deph * (1.0 - 3.0 * p / 4.0);
+    rc.dev_thr_host[3 * i + 0] = u32(px);
+    rc.dev_thr_host[3 * i + 1] = u32(px + py);
+    rc.dev_thr_host[3 * i + 2] = u32(px + py + pzz);
+    const double q1 = gamma / 2.0, q0 = 1.0 - q1;
+    jump[i] = u32(q1);
+    kraus[3 * i + 0] = 1.0 / std::sqrt(q0);
+    kraus[3 * i + 1] = std::sqrt(1.0 - gamma) / std::sqrt(q0);
+    kraus[3 * i + 2] = q1 > 0.0 ? std::sqrt(gamma / q1) : 0.0;
+  }
+  DTC_TRY(ensure(ctx->dev_thr, rc.dev_thr_host.size() * sizeof(uint32_t)));
+  DTC_TRY(ensure(ctx->dev_jump, jump.size() * sizeof(uint32_t)));
+  DTC_TRY(ensure(ctx->dev_kraus, kraus.size() * sizeof(double)));
+  DTC_HIP(hipMemcpyAsync(ctx->dev_thr.p, rc.dev_thr_host.data(),
+                         rc.dev_thr_host.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                         ctx->stream));
+  DTC_HIP(hipMemcpyAsync(ctx->dev_jump.p, jump.data(), jump.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice, ctx->stream));
+  DTC_HIP(hipMemcpyAsync(ctx->dev_kraus.p, kraus.data(), kraus.size() * sizeof(double),
+                         hipMemcpyHostToDevice, ctx->stream));
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  rc.device = true;
+  rc.noisy = 1;
+  rc.dev_thr = (const uint32_t*)ctx->dev_thr.p;
+  rc.dev_jump = (const uint32_t*)ctx->dev_jump.p;
+  rc.dev_kraus = (const double*)ctx->dev_kraus.p;
+  return DTC_OK;
+}
+
+int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                  const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset, int32_t n_traj,
+                  double* fwd, double* echo, double* zsite) {
   if (!ctx) return fail(DTC_EINVAL, "null ctx");
   DTC_TRY(check_problem(pr, nz));
   if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
@@ -773,6 +860,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   rc.noisy = nz->p > 0.0 ? 1 : 0;
   rc.row_kind = classify_rows(pr);
   thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  if (dv) DTC_TRY(setup_device_noise(ctx, pr, dv, rc));
   const Plan& pl = rc.pl;
   const int T = pr->T, L = pr->L;
   const int P = T - 1 + pr->t_offset;
@@ -781,7 +869,10 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
   const bool want_e = pr->want_echo != 0;
   const int n_obs_f = want_z ? 1 + L : 2;
   const int meas_f = want_z ? dtc::kMeasSites : dtc::kMeasProbe;
-  const double fac = std::pow(1.0 - nz->p, (double)nz->n_anc);
+  const double fac = dv ? dv->anc_factor : std::pow(1.0 - nz->p, (double)nz->n_anc);
+  // read-out: measured = ro_a * a + ro_b (identity without device noise)
+  const double ro_a = dv ? 1.0 - dv->readout_p01 - dv->readout_p10 : 1.0;
+  const double ro_b = dv ? dv->readout_p10 - dv->readout_p01 : 0.0;
 
   DTC_TRY(upload_tables(ctx, pr, pl));
 
@@ -846,6 +937,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
     std::vector<Launch> sched;
     if (P > 0) {
       Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
+      fw.post_after_d = !rc.device;
       while (!fw.done()) {
         PassSpec ps = next_pass(fw);
         const int p = ps.d_index;
@@ -888,7 +980,7 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
         const bool at_init = (t + pr->t_offset == 0);
         const double* vf = hv_f.data() + ((size_t)b * T + t) * n_obs_f;
         const double zj_f = at_init ? zinit : (want_z ? vf[1 + j] : vf[1]);
-        if (pr->want_fwd) fwd[(size_t)g * T + t] = fac * zinit * zj_f;
+        if (pr->want_fwd) fwd[(size_t)g * T + t] = ro_a * (fac * zinit * zj_f) + ro_b;
         if (want_z) {
           double* zo = zsite + ((size_t)g * T + t) * L;
           for (int i = 0; i < L; ++i)
@@ -896,12 +988,30 @@ int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint6
         }
         if (want_e) {
           const double zj_e = at_init ? zinit : hv_e[((size_t)b * T + t) * 2 + 1];
-          echo[(size_t)g * T + t] = fac * zinit * zj_e;
+          echo[(size_t)g * T + t] = ro_a * (fac * zinit * zj_e) + ro_b;
         }
       }
     }
   }
   return DTC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dtc_autocorr(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,
+                 int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
+                 double* zsite) {
+  return autocorr_impl(ctx, pr, nz, nullptr, seed, traj_offset, n_traj, fwd, echo, zsite);
+}
+
+int dtc_autocorr_device(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_noise* dv,
+                        uint64_t seed, int64_t traj_offset, int32_t n_traj, double* fwd,
+                        double* echo, double* zsite) {
+  if (!dv) return fail(DTC_EINVAL, "null device noise");
+  const dtc_noise nz{0.0, 0, 0};
+  return autocorr_impl(ctx, pr, &nz, dv, seed, traj_offset, n_traj, fwd, echo, zsite);
 }
 
 int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,

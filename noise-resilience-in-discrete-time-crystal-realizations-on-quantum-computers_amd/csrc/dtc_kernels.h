@@ -28,7 +28,10 @@ enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
-enum KickKind { kKindRX = 0, kKindRY = 1, kKindGen = 2 };
+// kKindRXU / kKindRYU: the same families without the unitary factoring (the
+// non-unitary kicks of device-like noise: Kraus x Pauli x RX stays of the
+// RX form), 4 flops per amplitude.
+enum KickKind { kKindRX = 0, kKindRY = 1, kKindGen = 2, kKindRXU = 3, kKindRYU = 4 };
 
 // One layer of single-site kicks on the sites of a pass.
 enum KickMode {
@@ -86,6 +89,12 @@ struct PrepArgs {
   uint32_t thr1, thr2, thr3;
   uint64_t seed;
   int noisy;
+  // device-like noise (null = depolarizing only): per logical site, Pauli
+  // thresholds [L][3], amplitude-damping jump threshold [L], and the
+  // importance-weighted Kraus factors [L][3] = (K0 00, K0 11, K1 01)
+  const uint32_t* dev_thr;
+  const uint32_t* dev_thr_jump;
+  const double* dev_kraus;
   KickRec* out;            // [n_pass][batch][kRecPerState]
 };
 

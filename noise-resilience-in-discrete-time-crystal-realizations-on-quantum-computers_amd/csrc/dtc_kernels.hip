@@ -47,6 +47,30 @@ __device__ __forceinline__ void bfly_general(double2& u, double2& v, const doubl
   v = nv;
 }
 
+// RX family, unfactored: [[a, i b], [i c, d]] (a, b, c, d real), 4 flops per amplitude
+__device__ __forceinline__ void bfly_rx(double2& u, double2& v, double a, double b, double c,
+                                        double d) {
+  double2 nu, nv;
+  nu.x = a * u.x - b * v.y;
+  nu.y = a * u.y + b * v.x;
+  nv.x = d * v.x - c * u.y;
+  nv.y = d * v.y + c * u.x;
+  u = nu;
+  v = nv;
+}
+
+// RY family, unfactored: [[a, b], [c, d]] real
+__device__ __forceinline__ void bfly_ry(double2& u, double2& v, double a, double b, double c,
+                                        double d) {
+  double2 nu, nv;
+  nu.x = a * u.x + b * v.x;
+  nu.y = a * u.y + b * v.y;
+  nv.x = c * u.x + d * v.x;
+  nv.y = c * u.y + d * v.y;
+  u = nu;
+  v = nv;
+}
+
 // m <- P m for Pauli code (1 X, 2 Y, 3 Z)
 __device__ __forceinline__ void pauli_left(double2* m, int pauli) {
   if (pauli == 1) {
@@ -105,7 +129,28 @@ __device__ void build_site_kick(const PrepArgs& P, const KickDesc& K, int site, 
     double2 gm[4] = {gp[0], gp[1], gp[2], gp[3]};
     if (inv) dagger(gm);
     mat_mul(m, gm, m);
-    if (P.noisy) {
+    if (P.dev_thr) {
+      // device-like noise: amplitude-damping Kraus operator drawn with fixed
+      // probabilities (q1 = gamma/2) and weighted by 1/sqrt(q) -- the
+      // trajectory stays linear and its mean is the exact channel -- then the
+      // composite dephasing + depolarizing Pauli
+      int jump = 0;
+      const int p = sample_device(P.seed, traj, K.stream, K.rng_period, (uint32_t)site,
+                                  (uint32_t)q, P.dev_thr + 3 * site, P.dev_thr_jump[site], &jump);
+      const double* kr = P.dev_kraus + 3 * site;
+      if (jump) {  // K1 = [[0, b], [0, 0]]: row 0 <- b row 1, row 1 <- 0
+        m[0] = make_double2(kr[2] * m[2].x, kr[2] * m[2].y);
+        m[1] = make_double2(kr[2] * m[3].x, kr[2] * m[3].y);
+        m[2] = make_double2(0.0, 0.0);
+        m[3] = make_double2(0.0, 0.0);
+      } else {     // K0 = diag(a0, a1)
+        m[0] = make_double2(kr[0] * m[0].x, kr[0] * m[0].y);
+        m[1] = make_double2(kr[0] * m[1].x, kr[0] * m[1].y);
+        m[2] = make_double2(kr[1] * m[2].x, kr[1] * m[2].y);
+        m[3] = make_double2(kr[1] * m[3].x, kr[1] * m[3].y);
+      }
+      pauli_left(m, p);
+    } else if (P.noisy) {
       int p = sample_pauli(P.seed, traj, K.stream, K.rng_period, (uint32_t)site, (uint32_t)q,
                            P.thr1, P.thr2, P.thr3);
       pauli_left(m, p);
@@ -147,7 +192,7 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
   sm.scale = 1.0;
   sm.var = 0;
   double a, b, c, d;
-  if (kind == kKindRX) {
+  if (kind == kKindRX || kind == kKindRXU) {
     const bool a_form = (m[0].y == 0.0 && m[1].x == 0.0 && m[2].x == 0.0 && m[3].y == 0.0);
     // B form [[i a, b], [c, i d]] = i [[a, -i b], [-i c, d]]
     a = a_form ? m[0].x : m[0].y;
@@ -155,7 +200,7 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
     c = a_form ? m[2].y : -m[2].x;
     d = a_form ? m[3].x : m[3].y;
     sm.k = a_form ? 0 : 1;
-  } else if (kind == kKindRY) {
+  } else if (kind == kKindRY || kind == kKindRYU) {
     const bool real = (m[0].y == 0.0 && m[1].y == 0.0 && m[2].y == 0.0 && m[3].y == 0.0);
     // imaginary form i [[a, b], [c, d]]
     a = real ? m[0].x : m[0].y;
@@ -165,6 +210,11 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
     sm.k = real ? 0 : 1;
   } else {
     for (int e = 0; e < 4; ++e) sm.m[e] = m[e];
+    return;
+  }
+  if (kind == kKindRXU || kind == kKindRYU) {  // unfactored: (a, b, c, d) as they are
+    sm.m[0] = make_double2(a, b);
+    sm.m[1] = make_double2(c, d);
     return;
   }
   // sigma from a d + b c = sigma (a^2 + b^2) (RX) or a d - b c (RY)
@@ -208,6 +258,9 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
           r.d[2 * e] = sm.m[e].x;
           r.d[2 * e + 1] = sm.m[e].y;
         }
+      } else if (pk.kind == kKindRXU || pk.kind == kKindRYU) {
+        r.d[0] = sm.m[0].x; r.d[1] = sm.m[0].y; r.d[2] = sm.m[1].x; r.d[3] = sm.m[1].y;
+        for (int e = 4; e < 8; ++e) r.d[e] = 0.0;
       } else {
         r.d[0] = sm.coef;
         r.i[1] = sm.var;
@@ -340,6 +393,14 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs&
 #pragma unroll
       for (int r = 0; r < kRegs; ++r)
         if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
+    } else if (KIND == kKindRXU || KIND == kKindRYU) {
+      const double a = R.d(k, 0), b = R.d(k, 1), c = R.d(k, 2), d = R.d(k, 3);
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        if (r & (1 << q)) continue;
+        if (KIND == kKindRXU) bfly_rx(v[r], v[r | (1 << q)], a, b, c, d);
+        else bfly_ry(v[r], v[r | (1 << q)], a, b, c, d);
+      }
     } else {
       const double f = R.d(k, 0);
       const int var = R.i(k, 1);
@@ -702,6 +763,8 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, hipStr
     case kKindRX: return launch_shape<NIBS, kKindRX>(a, grid, shape, stream);
     case kKindRY: return launch_shape<NIBS, kKindRY>(a, grid, shape, stream);
     case kKindGen: return launch_shape<NIBS, kKindGen>(a, grid, shape, stream);
+    case kKindRXU: return launch_shape<NIBS, kKindRXU>(a, grid, shape, stream);
+    case kKindRYU: return launch_shape<NIBS, kKindRYU>(a, grid, shape, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -47,6 +47,40 @@ DTC_HD uint32_t philox_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
   return c0;
 }
 
+// Philox4x32-10 words 0 and 1 of one counter (word 0 = philox_w0).
+DTC_HD void philox_w01(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                       uint32_t k1, uint32_t* w0, uint32_t* w1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(0xD2511F53u, c0, &hi0, &lo0);
+    mulhilo32(0xCD9E8D57u, c2, &hi1, &lo1);
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  *w0 = c0;
+  *w1 = c1;
+}
+
+// Device-like noise draw of one kick sub-gate (include/dtc.h dtc_device_noise):
+// word 0 -> Pauli against the site's thresholds (dephasing composed with
+// depolarizing), word 1 -> amplitude-damping jump iff w1 < thr_jump.
+DTC_HD int sample_device(uint64_t seed, uint64_t traj, uint32_t stream, uint32_t period,
+                         uint32_t site, uint32_t sub, const uint32_t* thr, uint32_t thr_jump,
+                         int* jump) {
+  uint32_t x, y;
+  philox_w01(site | (sub << 16), period, stream, (uint32_t)traj, (uint32_t)seed,
+             (uint32_t)(seed >> 32) ^ (uint32_t)(traj >> 32), &x, &y);
+  *jump = y < thr_jump ? 1 : 0;
+  if (x < thr[0]) return 1;
+  if (x < thr[1]) return 2;
+  if (x < thr[2]) return 3;
+  return 0;
+}
+
 // Pauli code: 0 = I, 1 = X, 2 = Y, 3 = Z.
 // thr[k] = round(k * p/4 * 2^32) for k = 1, 2, 3 (computed on the host).
 DTC_HD int sample_pauli(uint64_t seed, uint64_t traj, uint32_t stream,

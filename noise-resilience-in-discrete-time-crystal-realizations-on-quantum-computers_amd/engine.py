@@ -37,6 +37,7 @@ class SweepSpec:
     probe_site: int | None = None
     kick: np.ndarray | None = field(default=None, repr=False)
     init_mask_value: int | None = None   # explicit Z-basis prep (overrides initial_state)
+    device: object | None = field(default=None, repr=False)  # DeviceNoise (use_fakebackend=1)
 
     def __post_init__(self):
         self.hs = np.ascontiguousarray(np.atleast_2d(self.hs)[:, : self.L], dtype=np.float64)
@@ -155,11 +156,21 @@ class DtcEngine:
         echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
         zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
         pr = self._problem(spec, want_fwd, want_echo, batch, t_first)
-        nz = self._noise(spec)
-        _capi.check(self._lib.dtc_autocorr(
-            self._ctx, ctypes.byref(pr), ctypes.byref(nz), ctypes.c_uint64(seed),
-            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(fwd),
-            _capi.as_dptr(echo), _capi.as_dptr(zs)))
+        if spec.device is not None:
+            # device-like noise (include/dtc.h dtc_device_noise); spec.noise_prob unused
+            if spec.device.L != spec.L:
+                raise ValueError("device noise has a different number of sites")
+            dv = _capi.device_struct(spec.device)
+            _capi.check(self._lib.dtc_autocorr_device(
+                self._ctx, ctypes.byref(pr), ctypes.byref(dv), ctypes.c_uint64(seed),
+                ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(fwd),
+                _capi.as_dptr(echo), _capi.as_dptr(zs)))
+        else:
+            nz = self._noise(spec)
+            _capi.check(self._lib.dtc_autocorr(
+                self._ctx, ctypes.byref(pr), ctypes.byref(nz), ctypes.c_uint64(seed),
+                ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(fwd),
+                _capi.as_dptr(echo), _capi.as_dptr(zs)))
         out = {}
         if want_fwd:
             out["fwd"] = fwd

@@ -90,7 +90,15 @@ def run_sweep(spec: SweepSpec, n_traj: int | None = None, shots: int | None = No
             res[key] = None
             continue
         a = out[key]
-        res[key] = a.mean(axis=1) if shots is None else _shot_estimate(a, shots, rng)
+        if shots is None:
+            res[key] = a.mean(axis=1)
+        elif spec.device is not None:
+            # device-like noise: importance-weighted trajectories are not
+            # per-shot probabilities; draw the shots from the trajectory mean
+            m = np.clip((1.0 + a.mean(axis=1)) / 2.0, 0.0, 1.0)
+            res[key] = (2.0 * rng.binomial(shots, m) - shots) / shots
+        else:
+            res[key] = _shot_estimate(a, shots, rng)
     return SweepResult(res["fwd"], res["echo"], out.get("fwd"), out.get("echo"),
                        out.get("zsite"))
 

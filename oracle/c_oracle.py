@@ -32,6 +32,12 @@ class OrcNoise(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class OrcDeviceNoise(ctypes.Structure):
+    _fields_ = [("p_gate", _dp), ("t1_us", _dp), ("t2_us", _dp), ("gate_ns", ctypes.c_double),
+                ("anc_factor", ctypes.c_double), ("readout_p01", ctypes.c_double),
+                ("readout_p10", ctypes.c_double)]
+
+
 _lib = None
 
 
@@ -52,6 +58,9 @@ def lib():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32]
         _lib.orc_sample_pauli.restype = ctypes.c_int
+        _lib.orc_autocorr_device.argtypes = [
+            ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcDeviceNoise), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]
     return _lib
 
 
@@ -84,9 +93,19 @@ def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_e
     fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
     echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
     zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
-    rc = lib().orc_autocorr(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
-                            ctypes.byref(_noise(spec)), seed, traj_offset, n_traj, _ptr(fwd),
-                            _ptr(echo), _ptr(zs), n_threads)
+    dev = getattr(spec, "device", None)
+    if dev is not None:
+        dv = OrcDeviceNoise()
+        dv.p_gate, dv.t1_us, dv.t2_us = _ptr(dev.p_gate), _ptr(dev.t1_us), _ptr(dev.t2_us)
+        dv.gate_ns, dv.anc_factor = dev.gate_ns, dev.anc_factor
+        dv.readout_p01, dv.readout_p10 = dev.readout_p01, dev.readout_p10
+        rc = lib().orc_autocorr_device(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
+                                       ctypes.byref(dv), seed, traj_offset, n_traj, _ptr(fwd),
+                                       _ptr(echo), _ptr(zs), n_threads)
+    else:
+        rc = lib().orc_autocorr(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
+                                ctypes.byref(_noise(spec)), seed, traj_offset, n_traj, _ptr(fwd),
+                                _ptr(echo), _ptr(zs), n_threads)
     if rc != 0:
         raise RuntimeError(f"orc_autocorr failed: {rc}")
     out = {}

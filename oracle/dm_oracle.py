@@ -78,6 +78,21 @@ class DM:
             acc = acc + (p / 4) * self.t
         self.t = acc
 
+    def kraus(self, q, ops):
+        """rho <- sum_k K rho K^dagger on qubit q."""
+        base = self.t.copy()
+        acc = None
+        for K in ops:
+            self.t = base.copy()
+            a = self._ax(q)
+            t = np.tensordot(K, self.t, axes=([1], [a]))
+            t = np.moveaxis(t, 0, a)
+            b = self.n + a
+            t = np.tensordot(t, K.conj().T, axes=([b], [0]))
+            t = np.moveaxis(t, -1, b)
+            acc = t if acc is None else acc + t
+        self.t = acc
+
     def expect_z(self, q) -> complex:
         N = 1 << self.n
         m = self.t.reshape(N, N)
@@ -108,15 +123,34 @@ def _phase_rzz(n, a, b, theta):
     return np.exp(-0.5j * theta * zz)
 
 
+def device_channel(dm: DM, q: int, gamma: float, d: float, p: float):
+    """Device-like noise after a kick sub-gate (include/dtc.h dtc_device_noise):
+    amplitude damping gamma, dephasing Z w.p. d, depolarizing_error(p, 1)."""
+    K0 = np.array([[1, 0], [0, math.sqrt(1 - gamma)]], dtype=np.complex128)
+    K1 = np.array([[0, math.sqrt(gamma)], [0, 0]], dtype=np.complex128)
+    dm.kraus(q, [K0, K1])
+    dm.kraus(q, [math.sqrt(1 - d) * np.eye(2, dtype=np.complex128), math.sqrt(d) * PZ])
+    dm.depolarize(q, p)
+
+
+def _noise_after_kick(dm: DM, q: int, site: int, p):
+    """p: depolarizing parameter, or a list of per-site (gamma, d, p) channels."""
+    if isinstance(p, (list, tuple)):
+        device_channel(dm, q, *p[site])
+    else:
+        dm.depolarize(q, p)
+
+
 def _period(dm: DM, off: int, L: int, kick_gates, hs, phis, p, inverse=False):
     """One U_F (fast.py:111-121) on system qubits off..off+L-1, or its inverse
-    (fast.py:140-143).  ``kick_gates[i]`` = sub-gate list of site i."""
+    (fast.py:140-143).  ``kick_gates[i]`` = sub-gate list of site i; ``p`` =
+    depolarizing parameter or per-site device channels (device_channel)."""
     n = dm.n
     if not inverse:
         for i in range(L):
             for G in kick_gates[i]:
                 dm.u1(off + i, G)
-                dm.depolarize(off + i, p)
+                _noise_after_kick(dm, off + i, i, p)
         for i in list(range(0, L - 1, 2)) + list(range(1, L - 1, 2)):
             dm.diag(_phase_rzz(n, off + i, off + i + 1, phis[i]))
         for i in range(L):
@@ -129,7 +163,7 @@ def _period(dm: DM, off: int, L: int, kick_gates, hs, phis, p, inverse=False):
         for i in reversed(range(L)):
             for G in reversed(kick_gates[i]):
                 dm.u1(off + i, G.conj().T)
-                dm.depolarize(off + i, p)
+                _noise_after_kick(dm, off + i, i, p)
 
 
 def kick_gates_from_table(kick_row: np.ndarray):
@@ -219,6 +253,41 @@ def folded_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", probe=None, t_
             for k in range(s, 0, -1):
                 _period(e, 0, L, kick_gates_from_table(kick[k - 1]), hs, phis, p, inverse=True)
             echo[t] = fac * e.expect_z(j).real
+    return fwd, echo
+
+
+def device_folded_sweep(L, T, hs, phis, kick, dev, initial_state="vacuum", probe=None,
+                        t_offset=0, want_echo=True):
+    """Exact read-out A_fwd(t), A_echo(t) under device-like noise (``dev`` a
+    DeviceNoise): the folded L-qubit model with the per-site channel after
+    every kick sub-gate, the neel-prep X followed by its Pauli part only,
+    then anc_factor and the ancilla read-out map (include/dtc.h)."""
+    j = int(L / 2) if probe is None else probe
+    N = 1 << L
+    ch = dev.site_channels()
+    x = np.arange(N)
+    w = np.ones(N)
+    for i in range(L):
+        flipped = initial_state == "neel" and (i + 1) % 2 == 0
+        pf = (1 - ch[i][2] / 2) if flipped else 0.0   # X/Y after X undo the flip
+        b = (x >> i) & 1
+        w = w * np.where(b == 1, pf, 1 - pf)
+    zj = 1 - 2 * ((x >> j) & 1)
+    sigma = DM(L, np.diag(w * zj).astype(np.complex128))
+    fwd = np.zeros(T)
+    echo = np.zeros(T)
+    for s in range(T - 1 + t_offset + 1):
+        if s > 0:
+            _period(sigma, 0, L, kick_gates_from_table(kick[s - 1]), hs, phis, ch)
+        t = s - t_offset
+        if t < 0:
+            continue
+        fwd[t] = dev.readout(dev.anc_factor * sigma.expect_z(j).real)
+        if want_echo:
+            e = sigma.copy()
+            for k in range(s, 0, -1):
+                _period(e, 0, L, kick_gates_from_table(kick[k - 1]), hs, phis, ch, inverse=True)
+            echo[t] = dev.readout(dev.anc_factor * e.expect_z(j).real)
     return fwd, echo
 
 

@@ -58,6 +58,14 @@ typedef struct orc_noise {
   int32_t n_anc, reserved;
 } orc_noise;
 
+/* Same layout as dtc_device_noise in include/dtc.h. */
+typedef struct orc_device_noise {
+  const double* p_gate;
+  const double* t1_us;
+  const double* t2_us;
+  double gate_ns, anc_factor, readout_p01, readout_p10;
+} orc_device_noise;
+
 typedef struct { double re, im; } cpx;
 
 static inline cpx cx(double r, double i) { cpx z = {r, i}; return z; }
@@ -87,6 +95,10 @@ typedef struct {
   uint32_t thr[3];
   int noisy;
   uint64_t seed;
+  /* device-like noise (NULL dev_thr: depolarizing only) */
+  const uint32_t* dev_thr;   /* [L][3] */
+  const uint32_t* dev_jump;  /* [L] */
+  const double* dev_kraus;   /* [L][3] K0 00, K0 11, K1 01 */
 } orc_rng;
 
 static void orc_rng_init(orc_rng* r, double p, uint64_t seed) {
@@ -97,6 +109,9 @@ static void orc_rng_init(orc_rng* r, double p, uint64_t seed) {
   }
   r->noisy = p > 0.0;
   r->seed = seed;
+  r->dev_thr = NULL;
+  r->dev_jump = NULL;
+  r->dev_kraus = NULL;
 }
 
 /* 0 = I, 1 = X, 2 = Y, 3 = Z */
@@ -108,6 +123,20 @@ static int orc_pauli(const orc_rng* r, uint64_t traj, uint32_t stream, uint32_t 
   if (x < r->thr[0]) return 1;
   if (x < r->thr[1]) return 2;
   if (x < r->thr[2]) return 3;
+  return 0;
+}
+
+/* Device-like noise draw: Philox word 0 -> Pauli against the site's
+ * thresholds, word 1 -> amplitude-damping jump (include/dtc.h). */
+static int orc_device_draw(const orc_rng* r, uint64_t traj, uint32_t stream, uint32_t period,
+                           uint32_t site, uint32_t sub, uint32_t thr_jump, int* jump) {
+  uint32_t c[4] = {site | (sub << 16), period, stream, (uint32_t)traj};
+  uint32_t x = orc_philox(c, (uint32_t)r->seed, (uint32_t)(r->seed >> 32) ^ (uint32_t)(traj >> 32));
+  *jump = c[1] < thr_jump;
+  const uint32_t* t = r->dev_thr + 3 * site;
+  if (x < t[0]) return 1;
+  if (x < t[1]) return 2;
+  if (x < t[2]) return 3;
   return 0;
 }
 
@@ -150,6 +179,29 @@ static void gate_rz(cpx* psi, int L, int i, double theta) {
   for (size_t x = 0; x < n; ++x) psi[x] = cmul(psi[x], ((x >> i) & 1) ? dn : up);
 }
 
+/* The noise after one kick sub-gate: depolarizing Pauli (fast.py:84-86), or
+ * the device-like channel -- importance-weighted amplitude-damping Kraus
+ * operator, then the composite dephasing + depolarizing Pauli. */
+static void gate_noise(cpx* psi, int L, int site, const orc_rng* rng, uint64_t traj,
+                       uint32_t stream, uint32_t period, uint32_t q) {
+  if (rng->dev_thr) {
+    int jump = 0;
+    int pz = orc_device_draw(rng, traj, stream, period, (uint32_t)site, q, rng->dev_jump[site],
+                             &jump);
+    const double* kr = rng->dev_kraus + 3 * site;
+    cpx k[4];
+    if (jump) {
+      k[0] = cx(0, 0); k[1] = cx(kr[2], 0); k[2] = cx(0, 0); k[3] = cx(0, 0);
+    } else {
+      k[0] = cx(kr[0], 0); k[1] = cx(0, 0); k[2] = cx(0, 0); k[3] = cx(kr[1], 0);
+    }
+    gate_1q(psi, L, site, k);
+    gate_pauli(psi, L, site, pz);
+    return;
+  }
+  gate_pauli(psi, L, site, orc_pauli(rng, traj, stream, period, (uint32_t)site, q));
+}
+
 static void kick_gate(const orc_problem* pr, int row, int site, int q, int dagger, cpx m[4]) {
   const double* g = pr->kick + (((size_t)row * pr->L + site) * pr->n_sub + q) * 8;
   if (!dagger) {
@@ -172,7 +224,7 @@ static void period_forward(const orc_problem* pr, const orc_rng* rng, int inst, 
     for (int q = 0; q < pr->n_sub; ++q) {
       kick_gate(pr, period - 1, i, q, 0, m);
       gate_1q(psi, L, i, m);
-      gate_pauli(psi, L, i, orc_pauli(rng, traj, stream, (uint32_t)period, (uint32_t)i, (uint32_t)q));
+      gate_noise(psi, L, i, rng, traj, stream, (uint32_t)period, (uint32_t)q);
     }
   for (int i = 0; i < L - 1; i += 2) gate_rzz(psi, L, i, i + 1, phi[i]);
   for (int i = 1; i < L - 1; i += 2) gate_rzz(psi, L, i, i + 1, phi[i]);
@@ -196,7 +248,7 @@ static void period_inverse(const orc_problem* pr, const orc_rng* rng, int inst, 
     for (int q = 0; q < pr->n_sub; ++q) {
       kick_gate(pr, period - 1, i, pr->n_sub - 1 - q, 1, m);
       gate_1q(psi, L, i, m);
-      gate_pauli(psi, L, i, orc_pauli(rng, traj, stream, (uint32_t)step, (uint32_t)i, (uint32_t)q));
+      gate_noise(psi, L, i, rng, traj, stream, (uint32_t)step, (uint32_t)q);
     }
 }
 
@@ -214,7 +266,9 @@ static uint64_t init_mask(const orc_problem* pr, const orc_rng* rng, uint64_t tr
   uint64_t m = pr->init_mask;
   for (int i = 0; i < pr->L; ++i) {
     if (!((pr->init_mask >> i) & 1ull)) continue;
-    int pz = orc_pauli(rng, traj, 0xFFFFFFFFu, 0u, (uint32_t)i, 0u);
+    int jump = 0;
+    int pz = rng->dev_thr ? orc_device_draw(rng, traj, 0xFFFFFFFFu, 0u, (uint32_t)i, 0u, 0u, &jump)
+                          : orc_pauli(rng, traj, 0xFFFFFFFFu, 0u, (uint32_t)i, 0u);
     if (pz == 1 || pz == 2) m &= ~(1ull << i); /* X.X = I, Y.X ~ Z: back to |0> */
   }
   return m;
@@ -238,15 +292,14 @@ int orc_apply_periods(const orc_problem* pr, const orc_noise* nz, uint64_t seed,
 
 /* Trajectory schedule of the engine: forward prefix reused for every t, echo
  * at t branches off the forward state after p = t + t_offset periods. */
-int orc_autocorr(const orc_problem* pr, const orc_noise* nz, uint64_t seed, int64_t traj_offset,
-                 int32_t n_traj, double* fwd, double* echo, double* zsite, int32_t n_threads) {
+static int autocorr_run(const orc_problem* pr, const orc_rng* rngp, double fac, double ro_a,
+                        double ro_b, int64_t traj_offset, int32_t n_traj, double* fwd,
+                        double* echo, double* zsite, int32_t n_threads) {
   const int L = pr->L, T = pr->T;
   const int P = T - 1 + pr->t_offset;
   const size_t n = (size_t)1 << L;
-  const double fac = pow(1.0 - nz->p, (double)nz->n_anc);
   const int64_t S = (int64_t)pr->n_inst * n_traj;
-  orc_rng rng;
-  orc_rng_init(&rng, nz->p, seed);
+  const orc_rng rng = *rngp;
   int err = 0;
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
@@ -272,7 +325,7 @@ int orc_autocorr(const orc_problem* pr, const orc_noise* nz, uint64_t seed, int6
       if (t < 0 || t < pr->t_first) continue;
       if (pr->want_fwd || zsite) {
         measure_z(F, L, z);
-        if (pr->want_fwd) fwd[(size_t)g * T + t] = fac * zinit * z[1 + pr->probe_site];
+        if (pr->want_fwd) fwd[(size_t)g * T + t] = ro_a * (fac * zinit * z[1 + pr->probe_site]) + ro_b;
         if (zsite)
           for (int i = 0; i < L; ++i) zsite[((size_t)g * T + t) * L + i] = z[1 + i];
       }
@@ -281,12 +334,73 @@ int orc_autocorr(const orc_problem* pr, const orc_noise* nz, uint64_t seed, int6
         for (int k = 1; k <= p; ++k)
           period_inverse(pr, &rng, inst, E, p - k + 1, k, traj, (uint32_t)(1 + t));
         measure_z(E, L, z);
-        echo[(size_t)g * T + t] = fac * zinit * z[1 + pr->probe_site];
+        echo[(size_t)g * T + t] = ro_a * (fac * zinit * z[1 + pr->probe_site]) + ro_b;
       }
     }
     free(F); free(E); free(z);
   }
   return err ? -3 : 0;
+}
+
+int orc_autocorr(const orc_problem* pr, const orc_noise* nz, uint64_t seed, int64_t traj_offset,
+                 int32_t n_traj, double* fwd, double* echo, double* zsite, int32_t n_threads) {
+  orc_rng rng;
+  orc_rng_init(&rng, nz->p, seed);
+  return autocorr_run(pr, &rng, pow(1.0 - nz->p, (double)nz->n_anc), 1.0, 0.0, traj_offset,
+                      n_traj, fwd, echo, zsite, n_threads);
+}
+
+static uint32_t orc_u32(double prob) {
+  double v = floor(prob * 4294967296.0 + 0.5);
+  if (v >= 4294967295.0) v = 4294967295.0;
+  if (v < 0) v = 0;
+  return (uint32_t)v;
+}
+
+/* Device-like noise (include/dtc.h dtc_device_noise), restated: per site
+ * gamma = 1 - exp(-tg/T1); pure dephasing Z w.p. (1 - exp(-tg (1/T2 - 1/2T1)))/2
+ * (T2 <= 2 T1); composite with depolarizing(p): X, Y p/4, Z (1-d) p/4 + d (1-3p/4);
+ * jump w.p. q1 = gamma/2 with K1/sqrt(q1), else K0/sqrt(1 - q1). */
+int orc_autocorr_device(const orc_problem* pr, const orc_device_noise* dv, uint64_t seed,
+                        int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
+                        double* zsite, int32_t n_threads) {
+  const int L = pr->L;
+  uint32_t* thr = (uint32_t*)malloc(sizeof(uint32_t) * 3 * L);
+  uint32_t* jmp = (uint32_t*)malloc(sizeof(uint32_t) * L);
+  double* kr = (double*)malloc(sizeof(double) * 3 * L);
+  if (!thr || !jmp || !kr) { free(thr); free(jmp); free(kr); return -3; }
+  for (int i = 0; i < L; ++i) {
+    const double p = dv->p_gate[i];
+    const double t1 = dv->t1_us[i] > 0.0 ? dv->t1_us[i] * 1e3 : INFINITY;
+    double t2 = dv->t2_us[i] > 0.0 ? dv->t2_us[i] * 1e3 : INFINITY;
+    if (t2 > 2.0 * t1) t2 = 2.0 * t1;
+    const double tg = dv->gate_ns;
+    const double gamma = isinf(t1) ? 0.0 : 1.0 - exp(-tg / t1);
+    double rate = (isinf(t2) ? 0.0 : 1.0 / t2) - (isinf(t1) ? 0.0 : 0.5 / t1);
+    if (rate < 0.0) rate = 0.0;
+    const double d = 0.5 * (1.0 - exp(-tg * rate));
+    const double px = p / 4.0, py = p / 4.0;
+    const double pz = (1.0 - d) * p / 4.0 + d * (1.0 - 3.0 * p / 4.0);
+    thr[3 * i + 0] = orc_u32(px);
+    thr[3 * i + 1] = orc_u32(px + py);
+    thr[3 * i + 2] = orc_u32(px + py + pz);
+    const double q1 = gamma / 2.0, q0 = 1.0 - q1;
+    jmp[i] = orc_u32(q1);
+    kr[3 * i + 0] = 1.0 / sqrt(q0);
+    kr[3 * i + 1] = sqrt(1.0 - gamma) / sqrt(q0);
+    kr[3 * i + 2] = q1 > 0.0 ? sqrt(gamma / q1) : 0.0;
+  }
+  orc_rng rng;
+  orc_rng_init(&rng, 0.0, seed);
+  rng.noisy = 1;
+  rng.dev_thr = thr;
+  rng.dev_jump = jmp;
+  rng.dev_kraus = kr;
+  const int rc = autocorr_run(pr, &rng, dv->anc_factor, 1.0 - dv->readout_p01 - dv->readout_p10,
+                              dv->readout_p10 - dv->readout_p01, traj_offset, n_traj, fwd, echo,
+                              zsite, n_threads);
+  free(thr); free(jmp); free(kr);
+  return rc;
 }
 
 /* Exposed for the RNG contract test. */

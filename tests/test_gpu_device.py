@@ -1,0 +1,123 @@
+"""Device-like noise on the HIP engine (dtc_autocorr_device) vs the C oracle.
+
+Same RNG contract on both sides (Philox word 0: Pauli, word 1: amplitude-
+damping jump), so every importance-weighted trajectory is the same random
+non-unitary circuit: per-trajectory values agree to 1e-10.  The engine's
+trajectory means are also checked against the exact density matrix (L=4).
+Parity with the reference's FakeBrisbane runs is unpinned (calibration data
+unavailable offline).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle, dm_oracle
+from tests.helpers import random_disorder
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def harsh_device(pkg, L):
+    return pkg.DeviceNoise(p_gate=np.full(L, 0.02), t1_us=np.linspace(1.5, 3.0, L),
+                           t2_us=np.linspace(1.0, 4.0, L), gate_ns=120.0, anc_factor=0.9,
+                           readout_p01=0.02, readout_p10=0.035)
+
+
+@pytest.mark.parametrize("L,T,n_traj,state,pol,toff", [
+    (4, 10, 6, "vacuum", "x", 0),
+    (6, 8, 4, "neel", "xy", 0),
+    (12, 7, 3, "vacuum", "y", 1),
+    (14, 6, 3, "neel", "circular_left", 0),
+    (20, 5, 2, "vacuum", "x", 0),
+])
+def test_device_engine_matches_oracle(pkg, engine, L, T, n_traj, state, pol, toff):
+    rng = np.random.default_rng(L * 7 + T)
+    hs, phis = random_disorder(rng, L, 2 if L < 12 else 1)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, polarization=pol,
+                         initial_state=state, t_offset=toff, device=harsh_device(pkg, L))
+    got = engine.autocorr(spec, n_traj, seed=21, want_zsite=True)
+    ref = c_oracle.autocorr(spec, n_traj, seed=21, want_zsite=True)
+    for k in ref:
+        err = float(np.abs(got[k] - ref[k]).max())
+        assert err < 1e-10, (k, err)
+
+
+def test_device_standin_L20_matches_oracle(pkg, engine, golden):
+    cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data", "device_standin_L20.json"))
+    d = golden["disorder"]["L20"]
+    spec = pkg.SweepSpec(L=20, T=4, hs=np.array(d["hs"])[:1], phis=np.array(d["phis"])[:1],
+                         g=0.97, device=cal.device_noise(20))
+    got = engine.autocorr(spec, 2, seed=5)
+    ref = c_oracle.autocorr(spec, 2, seed=5)
+    for k in ref:
+        assert float(np.abs(got[k] - ref[k]).max()) < 1e-10
+
+
+def test_device_batch_invariance(pkg, engine):
+    rng = np.random.default_rng(2)
+    hs, phis = random_disorder(rng, 13)
+    spec = pkg.SweepSpec(L=13, T=5, hs=hs, phis=phis, device=harsh_device(pkg, 13))
+    a = engine.autocorr(spec, 6, seed=3, batch=6)
+    b = engine.autocorr(spec, 6, seed=3, batch=2)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
+
+
+def test_device_means_match_exact_dm(pkg, engine):
+    rng = np.random.default_rng(11)
+    L, T = 4, 6
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.9, device=harsh_device(pkg, L))
+    fe, ee = dm_oracle.device_folded_sweep(L, T, spec.hs[0], spec.phis[0], spec.kick,
+                                           spec.device)
+    n = 8192
+    out = engine.autocorr(spec, n, seed=123)
+    for key, exact in (("fwd", fe), ("echo", ee)):
+        a = out[key][0]
+        se = a.std(axis=0, ddof=1) / np.sqrt(n) + 1e-12
+        z = (a.mean(axis=0) - exact) / se
+        assert np.max(np.abs(z)) < 4.5, (key, z)
+
+
+def test_cli_use_fakebackend(pkg, golden, tmp_path):
+    """dtc_autocorr.py --use_fakebackend 1: device-like noise from the stand-in
+    calibration, fast.py's folder/file names (fakebackend1)."""
+    import pandas as pd
+
+    d = golden["disorder"]["L4"]
+    dis = tmp_path / "dis"
+    dis.mkdir()
+    pd.DataFrame(d["hs"]).to_csv(dis / "hs_L4.csv", index=False)
+    pd.DataFrame(d["phis"]).to_csv(dis / "phis_L4.csv", index=False)
+    out = tmp_path / "out"
+    rc = pkg.cli.main(["--L", "4", "--tf", "5", "--use_fakebackend", "1", "--shots", "0",
+                       "--trajectories", "64", "--disorder_folder", str(dis),
+                       "--out_dir", str(out)])
+    assert rc == 0
+    files = list((out / "autocorr_data_L4_noiseprob0.05_fakebackend1").glob("autocorr_data_*.csv"))
+    assert len(files) == 1
+    df = pd.read_csv(files[0])
+    assert list(df.columns) == ["time", "av_autocorr", "av_autocorr_echo", "sqrt_av_autocorr_echo"]
+    # t = 0: no kicks -> read-out of anc_factor * 1
+    cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data", "device_standin_L20.json"))
+    dev = cal.device_noise(4)
+    assert df["av_autocorr"][0] == pytest.approx(dev.readout(dev.anc_factor), abs=1e-12)
+
+
+def test_aer_facade_from_backend(pkg):
+    """NoiseModel.from_backend(FakeDevice(...)) -> AerSimulator.run(...) (fast.py:77-79,
+    152-156, 211-212 with a calibration file instead of FakeBrisbane)."""
+    backend = pkg.aer.FakeDevice(os.path.join(ROOT, "data", "device_standin_L20.json"))
+    nm = pkg.NoiseModel.from_backend(backend)
+    circ = pkg.circuit.dtc_circuit(4, 0, np.zeros(4), np.zeros(3),
+                                   lambda step: [[("rx", np.pi * 0.97)] for _ in range(4)])
+    sim = pkg.AerSimulator(noise_model=nm, device="GPU", seed_simulator=1)
+    counts = sim.run(circ, shots=1000).result().get_counts()
+    dev = backend.calibration.device_noise(4)
+    a = dev.readout(dev.anc_factor)
+    n0 = counts.get("0", 0)
+    assert abs(n0 / 1000 - (1 + a) / 2) < 5 * np.sqrt(0.25 / 1000)
+    with pytest.raises(NotImplementedError):
+        pkg.NoiseModel.from_backend(object())
