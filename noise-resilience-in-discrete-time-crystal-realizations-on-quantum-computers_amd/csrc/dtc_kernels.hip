@@ -618,25 +618,48 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
       zr[j] = z;
     }
-    double tot = wave_sum(ptot);
-    if (lane == 0) s_red[wave][0] = tot;
     const bool probe_only = A.meas == kMeasProbe;
-    const int n_z = probe_only ? 1 : A.L_real;
     auto tile_bit = [&](int site) {
       return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
-    for (int i = 0; i < n_z; ++i) {
-      const int site = probe_only ? A.probe : i;
+    // s_red slots: 0 wave total; probe mode: 1 probe site; site/energy modes:
+    // 1..6 parity sums over lane bits 0..5, 7..10 register-bit site sums,
+    // 11.. bond correlators
+    constexpr int kSlotLane = 1, kSlotReg = 7, kSlotBond = 11;
+    if (probe_only) {
+      const double tot = wave_sum(ptot);
+      if (lane == 0) s_red[wave][0] = tot;
+      const int site = A.probe;
       const int tb = tile_bit(site);
-      if (tb < 0) continue;
-      const int j = tb - 4 * LAY;
-      double z;
-      if (j >= 0 && j < 4)
-        z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
-      else
-        z = ((x0 >> site) & 1) ? -ptot : ptot;
-      z = wave_sum(z);
-      if (lane == 0) s_red[wave][1 + i] = z;
+      if (tb >= 0) {
+        const int j = tb - 4 * LAY;
+        double z;
+        if (j >= 0 && j < 4)
+          z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
+        else
+          z = ((x0 >> site) & 1) ? -ptot : ptot;
+        z = wave_sum(z);
+        if (lane == 0) s_red[wave][1] = z;
+      }
+    } else {
+      // every in-tile site at once: a 6-stage Walsh-Hadamard transform of the
+      // lane totals leaves sum_t (-1)^bit_k(t) ptot(t) in lane 2^k and the
+      // wave total in lane 0 (6 shuffles instead of one reduction per site)
+      double h = ptot;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double o = __shfl_xor(h, 1 << k, 64);
+        h = ((lane >> k) & 1) ? o - h : h + o;
+      }
+      if (lane == 0) s_red[wave][0] = h;
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (lane == (1 << k)) s_red[wave][kSlotLane + k] = h;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double z = wave_sum(zr[j]);
+        if (lane == 0) s_red[wave][kSlotReg + j] = z;
+      }
     }
     if (A.meas == kMeasEnergy) {
       // bond correlators <Z_i Z_i+1>: sign per amplitude, generic reduction
@@ -648,17 +671,40 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
           z += (((x >> i) ^ (x >> (i + 1))) & 1) ? -pr[r] : pr[r];
         }
         z = wave_sum(z);
-        if (lane == 0) s_red[wave][1 + A.L_real + i] = z;
+        if (lane == 0) s_red[wave][kSlotBond + i] = z;
       }
     }
     __syncthreads();
     if (t < A.n_obs) {
-      const int site = probe_only ? A.probe : t - 1;
-      const bool is_site = t >= 1 && t <= n_z;
-      const int ws = (!is_site || tile_bit(site) >= 0) ? t : 0;
+      constexpr int NW = kThreads / 64;
       double acc = 0.0;
-      for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
-      if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
+      if (probe_only) {
+        const int site = A.probe;
+        const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
+        for (int w = 0; w < NW; ++w) acc += s_red[w][ws];
+        if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
+      } else if (t == 0) {
+        for (int w = 0; w < NW; ++w) acc += s_red[w][0];
+      } else if (t <= A.L_real) {
+        const int site = t - 1;
+        const int tb = tile_bit(site);
+        if (tb < 0) {  // one sign over the tile
+          for (int w = 0; w < NW; ++w) acc += s_red[w][0];
+          if ((M.tbase >> site) & 1) acc = -acc;
+        } else if (tb >= 4 * LAY && tb < 4 * LAY + 4) {  // register bit
+          for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotReg + tb - 4 * LAY];
+        } else {  // thread bit q of ybase<LAY>
+          const int q = LAY == 2 ? tb : (LAY == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
+          if (q < 6) {
+            for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotLane + q];
+          } else {  // wave bit
+            for (int w = 0; w < NW; ++w)
+              acc += ((w >> (q - 6)) & 1) ? -s_red[w][0] : s_red[w][0];
+          }
+        }
+      } else {
+        for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotBond + t - 1 - A.L_real];
+      }
       acc *= inv_w2;
       A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
     }
