@@ -23,6 +23,12 @@ $(ORACLE): oracle/dtc_oracle.c
 resource-usage: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage $(SRCS) -o /tmp/dtc_ru.so
 
+# Development-only build (instrumentation; never the product): per-workgroup
+# phase timing, loaded with DTC_LIB=build/libdtc_timing.so by tools/phase_timing.py.
+build/libdtc_timing.so: $(SRCS) $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DDTC_PHASE_TIMING=3 $(SRCS) -o $@
+
 clean:
 	rm -f $(LIB) $(ORACLE)
 
