@@ -257,6 +257,7 @@ struct Chain {
   std::vector<int> kc;      // layers applied per group
   int nd = 0;               // diagonals applied
   bool post_after_d = true; // a pass that applies D may start the next layer
+  std::vector<int> prio;    // tie-break between groups with equal kc (lower first); empty = index
   int n() const { return (int)X.size() - 1; }
   int n_d() const { return trailing_d ? n() + 1 : n(); }
   bool done() const {
@@ -276,7 +277,11 @@ struct PassSpec {
 
 // Emit the next pass of a chain (greedy, deterministic).
 PassSpec next_pass(Chain& ch) {
-  const int G = (int)(std::min_element(ch.kc.begin(), ch.kc.end()) - ch.kc.begin());
+  int G = 0;
+  for (int g = 1; g < (int)ch.kc.size(); ++g) {
+    const int pg = ch.prio.empty() ? g : ch.prio[g], pG = ch.prio.empty() ? G : ch.prio[G];
+    if (ch.kc[g] < ch.kc[G] || (ch.kc[g] == ch.kc[G] && pg < pG)) G = g;
+  }
   PassSpec ps{G, no_kick(), no_kick(), dtc::kDiagNone, ch.nd};
   const int n = ch.n();
   if (ch.kc[G] == ch.nd && ch.kc[G] <= n) ps.pre = ch.X[ch.kc[G]++];
@@ -938,6 +943,13 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     if (P > 0) {
       Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
       fw.post_after_d = !rc.device;
+      // start on a group without the probe site: every echo chain then ends
+      // with its kick-only pass on such a group, which the probe does not need
+      // (two groups: the closing groups alternate with p, see below)
+      fw.prio.resize(pl.groups.size());
+      for (size_t g = 0; g < pl.groups.size(); ++g)
+        fw.prio[g] = (int)g + (((group_bits(pl.groups[g]) >> pr->probe_site) & 1ull)
+                                   ? (int)pl.groups.size() : 0);
       while (!fw.done()) {
         PassSpec ps = next_pass(fw);
         const int p = ps.d_index;
@@ -952,14 +964,25 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > p;
         Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
         const double2* src = F;
+        const size_t chain0 = sched.size();
         while (!ec.done()) {
           PassSpec es = next_pass(ec);
-          const bool last = ec.done();
-          sched.push_back(Launch{es, src, E, last ? dtc::kMeasProbe : dtc::kMeasNone, 1, 2,
-                                 last ? (double*)ctx->vals_e.p + (size_t)t * 2 : nullptr,
-                                 (int64_t)T * 2});
+          sched.push_back(Launch{es, src, E, dtc::kMeasNone, 1, 2, nullptr, (int64_t)T * 2});
           src = E;
         }
+        // A chain that ends with a kick-only pass on a group without the probe
+        // site: unitary single-site kicks on other sites leave <Z_j> unchanged
+        // (K_i^+ Z_j K_i = Z_j), so that pass is dropped and the probe is read
+        // after the previous one.  Not for device-like noise: its Kraus kicks
+        // are not unitary and change the trajectory weight.
+        if (!rc.device && sched.size() - chain0 >= 2) {
+          const Launch& l = sched.back();
+          const bool kick_only = l.ps.diag == dtc::kDiagNone && !l.ps.post.enabled;
+          if (kick_only && !((group_bits(pl.groups[l.ps.group]) >> pr->probe_site) & 1ull))
+            sched.pop_back();
+        }
+        sched.back().meas_mode = dtc::kMeasProbe;
+        sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;
       }
     }
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
