@@ -30,24 +30,8 @@ DTC_HD void mulhilo32(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
   *lo = (uint32_t)p;
 }
 
-// Philox4x32 with 10 rounds (Salmon et al., SC'11).  Returns word 0.
-DTC_HD uint32_t philox_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                          uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hi0, lo0, hi1, lo1;
-    mulhilo32(0xD2511F53u, c0, &hi0, &lo0);
-    mulhilo32(0xCD9E8D57u, c2, &hi1, &lo1);
-    uint32_t n0 = hi1 ^ c1 ^ k0;
-    uint32_t n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c0;
-}
-
-// Philox4x32-10 words 0 and 1 of one counter (word 0 = philox_w0).
+// Philox4x32 with 10 rounds (Salmon et al., SC'11): words 0 and 1 of the
+// output block for counter (c0..c3) and key (k0, k1).
 DTC_HD void philox_w01(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                        uint32_t k1, uint32_t* w0, uint32_t* w1) {
 #pragma unroll
@@ -63,6 +47,14 @@ DTC_HD void philox_w01(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint3
   }
   *w0 = c0;
   *w1 = c1;
+}
+
+// Word 0 only.
+DTC_HD uint32_t philox_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                          uint32_t k0, uint32_t k1) {
+  uint32_t w0, w1;
+  philox_w01(c0, c1, c2, c3, k0, k1, &w0, &w1);
+  return w0;
 }
 
 // Device-like noise draw of one kick sub-gate (include/dtc.h dtc_device_noise):
