@@ -108,8 +108,9 @@ def main():
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-traj", type=int, default=0, help="0 = one per host thread")
-    ap.add_argument("--cpu-tf", type=int, default=8)
+    ap.add_argument("--cpu-traj", type=int, default=0, help="0 = two per host thread")
+    ap.add_argument("--cpu-tf", type=int, default=10,
+                    help="time points of the CPU sample (about 10 s on 16 host threads)")
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
                          "device-like noise (stand-in calibration, data/"
@@ -208,7 +209,7 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not c3:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        ntr = args.cpu_traj or threads
+        ntr = args.cpu_traj or 2 * threads
         cpu = cpu_baseline(spec, ntr, args.cpu_tf, threads)
 
     info = eng.device_info()
