@@ -121,3 +121,38 @@ def test_aer_facade_from_backend(pkg):
     assert abs(n0 / 1000 - (1 + a) / 2) < 5 * np.sqrt(0.25 / 1000)
     with pytest.raises(NotImplementedError):
         pkg.NoiseModel.from_backend(object())
+
+
+def test_device_error_paths(pkg, engine):
+    rng = np.random.default_rng(0)
+    hs, phis = random_disorder(rng, 6)
+    bad_p = pkg.DeviceNoise(p_gate=np.full(6, 2.0), t1_us=np.full(6, 100.0),
+                            t2_us=np.full(6, 100.0), gate_ns=60.0)
+    spec = pkg.SweepSpec(L=6, T=3, hs=hs, phis=phis, device=bad_p)
+    with pytest.raises(pkg._capi.DtcError, match="p_gate"):
+        engine.autocorr(spec, 2)
+    bad_ro = pkg.DeviceNoise(p_gate=np.full(6, 0.01), t1_us=np.full(6, 100.0),
+                             t2_us=np.full(6, 100.0), gate_ns=60.0, readout_p01=1.5)
+    with pytest.raises(pkg._capi.DtcError, match="read-out"):
+        engine.autocorr(pkg.SweepSpec(L=6, T=3, hs=hs, phis=phis, device=bad_ro), 2)
+    wrong_L = pkg.DeviceNoise(p_gate=np.full(5, 0.01), t1_us=np.full(5, 100.0),
+                              t2_us=np.full(5, 100.0), gate_ns=60.0)
+    with pytest.raises(ValueError):
+        engine.autocorr(pkg.SweepSpec(L=6, T=3, hs=hs, phis=phis, device=wrong_L), 2)
+
+
+def test_device_infinite_t1_is_pauli_noise(pkg, engine):
+    """T1 = T2 = inf: the device channel is depolarizing only; with anc_factor
+    (1-p)^6 and no read-out error it equals dtc_autocorr's exact mean (DM)."""
+    rng = np.random.default_rng(4)
+    L, T, p = 4, 6, 0.05
+    hs, phis = random_disorder(rng, L)
+    dev = pkg.DeviceNoise(p_gate=np.full(L, p), t1_us=np.zeros(L), t2_us=np.zeros(L),
+                          gate_ns=120.0, anc_factor=(1 - p) ** 6)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, device=dev)
+    fe, ee = dm_oracle.folded_sweep(L, T, spec.hs[0], spec.phis[0], spec.kick, p)
+    out = engine.autocorr(spec, 4096, seed=17)
+    for key, exact in (("fwd", fe), ("echo", ee)):
+        a = out[key][0]
+        z = (a.mean(axis=0) - exact) / (a.std(axis=0, ddof=1) / np.sqrt(4096) + 1e-12)
+        assert np.max(np.abs(z)) < 4.5, (key, z)
