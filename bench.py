@@ -60,17 +60,17 @@ def periods_per_traj(T, t_offset=0):
     return P + echo
 
 
-def cpu_baseline(spec, n_traj, T_sample, threads):
+def cpu_baseline(spec, n_traj, T_sample, threads, t_offset=0):
     """Time the C oracle (gate-by-gate restatement) on the host cores."""
     from oracle import c_oracle
 
     pkg = importlib.import_module(PKG)
     s = pkg.SweepSpec(L=spec.L, T=T_sample, hs=spec.hs, phis=spec.phis, g=spec.g,
-                      noise_prob=spec.noise_prob, use_noise=spec.use_noise)
+                      noise_prob=spec.noise_prob, use_noise=spec.use_noise, t_offset=t_offset)
     t0 = time.perf_counter()
     c_oracle.autocorr(s, n_traj, seed=0xC0FFEE, n_threads=threads)
     dt = time.perf_counter() - t0
-    work = n_traj * periods_per_traj(T_sample)
+    work = n_traj * periods_per_traj(T_sample, t_offset)
     return {
         "value": work / dt,
         "unit": "periods*instances/s",
@@ -111,12 +111,15 @@ def main():
     ap.add_argument("--cpu-traj", type=int, default=0, help="0 = two per host thread")
     ap.add_argument("--cpu-tf", type=int, default=10,
                     help="time points of the CPU sample (about 10 s on 16 host threads)")
-    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2",
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "energy", "ctrl"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
                          "device-like noise (stand-in calibration, data/"
                          "device_standin_L20.json), 1024 trajectories per step; c4: L=28 "
                          "noiseless disorder sweep, instances sharded over ranks; c5: one "
-                         "L=34 state sharded over the ranks (1 GPU: --L 31, 8 virtual ranks)")
+                         "L=34 state sharded over the ranks (1 GPU: --L 31, 8 virtual ranks); "
+                         "energy: the energy observable path (§8(f)1); ctrl: the real-time "
+                         "adaptive-g controller loop (§8(f)2)")
+    ap.add_argument("--ctrl-tf", type=int, default=20, help="ctrl: time points of the loop")
     ap.add_argument("--shard-bits", type=int, default=3, help="c5: log2 of the shard count")
     ap.add_argument("--instances", type=int, default=32, help="c4: instances per step per GPU")
     args = ap.parse_args()
@@ -124,6 +127,10 @@ def main():
         return main_c4(args)
     if args.config == "c5":
         return main_c5(args)
+    if args.config == "energy":
+        return main_energy(args)
+    if args.config == "ctrl":
+        return main_ctrl(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -470,6 +477,219 @@ def main_c5(args):
         "kat_cos_pi_g": float(np.cos(np.pi * 0.97)),
         "device": eng.device_info()["name"],
     }
+    print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def _init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    torch.cuda.set_device(local_rank if world > 1 else 0)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+    return world, rank, local_rank, dist
+
+
+def _timed(eng, dist, warmup, steps, step, reduce_buf):
+    """Warmup, then exactly `steps` steps between barrier + synchronize; the
+    per-rank accumulator `reduce_buf` (numpy) is all-reduced once inside the
+    timed region.  Returns (max-over-ranks seconds, reduced array, kernel stats)."""
+    import torch
+
+    for i in range(warmup):
+        step(i)
+    reduce_buf[...] = 0
+    eng.reset_stats()
+    eng.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    acc = torch.from_numpy(reduce_buf).cuda()
+    if dist:
+        dist.all_reduce(acc)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    stats = eng.kernel_stats()
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()), acc.cpu().numpy(), stats
+
+
+def _pass_kernels(stats, elapsed):
+    """Roofline of the K-D-K pass kernel (stats kind 0) from the engine's HIP
+    events, plus the other kinds' totals."""
+    lo_s, hi_s = stats[0], stats[1]
+    avg_lo = lo_s["total_ms"] / max(1, lo_s["launches"]) / 1e3
+    avg_hi = hi_s["total_ms"] / max(1, hi_s["launches"]) / 1e3
+    lo_b = lo_s["bytes"] / max(1, lo_s["launches"])
+    hi_b = hi_s["bytes"] / max(1, hi_s["launches"])
+    achieved = lo_b / avg_lo / 1e9 if lo_s["launches"] else 0.0
+    roof = {"bound": "hbm", "kernel": "dtc_kdk_pass", "achieved": achieved,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "frac_of_box_copy": achieved / BOX_COPY_GBS, "traffic": None,
+            "algorithmic_bytes_per_launch": lo_b, "avg_launch_ms": avg_lo * 1e3,
+            "launches": lo_s["launches"]}
+    kern = {"kdk_pass": {"launches": lo_s["launches"], "avg_ms": avg_lo * 1e3},
+            "kick_pass": {"launches": hi_s["launches"], "avg_ms": avg_hi * 1e3,
+                          "GBps": hi_b / avg_hi / 1e9 if hi_s["launches"] else None},
+            "reduce": {"launches": stats[2]["launches"], "total_ms": stats[2]["total_ms"]},
+            "kernel_time_frac": sum(stats[k]["total_ms"] for k in range(4)) / (elapsed * 1e3)}
+    return roof, kern
+
+
+def _host_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+
+def main_energy(args):
+    """SURVEY.md §8(f)1, the energy path (…-fast-energy.py:136-173 at L=20):
+    per-trajectory <Z_i>, <Z_i Z_i+1>, <X_i> after every period of the noisy
+    forward sweep (dtc_energy), L=20, g=0.97, p=0.05, vacuum, tf=30.  One step
+    = `--batch` trajectories per GPU; <H(t)>/L of instance 0 is formed on the
+    host from the trajectory means (energy.energy_from_observables).  Value =
+    trajectories x (tf-1) periods per second over all ranks (each period also
+    measures Z, ZZ and X, the X basis by one extra kick pass per site group)."""
+    world, rank, local_rank, dist = _init_dist()
+    pkg = importlib.import_module(PKG)
+    L, T, B = args.L, args.tf, args.batch
+    hs, phis = load_disorder_row(L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.97, noise_prob=0.05, use_noise=1)
+    eng = pkg.DtcEngine(local_rank)
+    sums = np.zeros((3, T, L))
+
+    def step(i):
+        off = (rank * (args.warmup + args.steps) + i) * B
+        obs = eng.energy(spec, B, traj_offset=off, batch=B)
+        sums[0] += obs["z"][0].sum(axis=0)
+        sums[1, :, :L - 1] += obs["zz"][0].sum(axis=0)
+        sums[2] += obs["x"][0].sum(axis=0)
+
+    elapsed, acc, stats = _timed(eng, dist, args.warmup, args.steps, step, sums)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    n = world * args.steps * B
+    mean = {"z": acc[0] / n, "zz": acc[1, :, :L - 1] / n, "x": acc[2] / n}
+    e_t = pkg.energy.energy_from_observables(mean, L, 0.97, hs[0], phis[0], "full") / L
+    roof, kern = _pass_kernels(stats, elapsed)
+    roof["kernel"] = "dtc_kdk_pass (forward period, Z/ZZ reduction fused in the epilogue)"
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_energy(spec, args.cpu_traj or _host_threads(),
+                                  min(args.cpu_tf, 4), _host_threads())
+    res = {
+        "metric": "Floquet-periods×trajectories/sec at L=20 with <Z_i>,<Z_iZ_i+1>,<X_i> per "
+                  "period (energy path); RZZ-kernel HBM GB/s vs peak",
+        "value": n * (T - 1) / elapsed, "unit": "periods*trajectories/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (disorder row 0 of hs/phis_L20.csv)",
+        "config": {"workload": (f"energy path (§8(f)1): L={L}, g=0.97, p=0.05, vacuum, tf={T}, "
+                                f"{B} noisy trajectories per step per GPU, Z/ZZ/X every period"),
+                   "L": L, "tf": T, "trajectories_per_step_per_gpu": B,
+                   "parallelism": f"traj-sharded x{world}"},
+        "roofline": roof, "kernels": kern,
+        "energy_per_site_t0_3": [float(x) for x in e_t[:4]],
+        "device": eng.device_info()["name"],
+    }
+    if cpu:
+        res["cpu_baseline"] = cpu
+    print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_energy(spec, n_traj, T_sample, threads):
+    """oracle/energy_oracle.py (C gate-by-gate periods + numpy observables),
+    one trajectory per host thread."""
+    import dataclasses
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import energy_oracle
+
+    s = dataclasses.replace(spec, T=T_sample)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda tr: energy_oracle.trajectory_energy(s, 0, tr), range(n_traj)))
+    dt = time.perf_counter() - t0
+    work = n_traj * (T_sample - 1)
+    return {"value": work / dt, "unit": "periods*trajectories/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle/energy_oracle.py (C oracle periods + numpy Z/ZZ/X): L={spec.L}, "
+                       f"{n_traj} trajectories x T={T_sample} = {work} periods in {dt:.1f} s")}
+
+
+def main_ctrl(args):
+    """SURVEY.md §8(f)2, the real-time adaptive-g controller
+    (…-controlled-g.py:423-532) on the committed L=20 configuration
+    (controlled-autocorr_data_L20: g_initial=0.84, p=0.05, 1024 shots,
+    tf=20): one step = one instance's closed loop, at every t one engine call
+    for the forward and echo values of the g history (t+1 periods each) and a
+    host feedback update.  Instances (disorder rows) are sharded over ranks.
+    Value = period applications x trajectories per second."""
+    world, rank, local_rank, dist = _init_dist()
+    pkg = importlib.import_module(PKG)
+    L, T, shots = args.L, args.ctrl_tf, 1024
+    eng = pkg.DtcEngine(local_rank)
+    cfg = pkg.control.ControllerConfig()
+    hs, phis = load_disorder_row(L)
+    res_g = np.zeros((1, T))
+
+    def step(i):
+        r = pkg.control.realtime_adaptive(L, T, hs, phis, 0.84, cfg, noise_prob=0.05,
+                                          shots=shots, seed=0x5EED0001 + 7919 * (i * world + rank),
+                                          engine=eng)
+        res_g[0] += r.g[0]
+
+    elapsed, acc, stats = _timed(eng, dist, args.warmup, args.steps, step, res_g)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    per_loop = shots * sum(2 * (t + 1) for t in range(T))
+    n_loops = world * args.steps
+    roof, kern = _pass_kernels(stats, elapsed)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        hs_, phis_ = load_disorder_row(L)
+        s = pkg.SweepSpec(L=L, T=args.cpu_tf, hs=hs_, phis=phis_, g=0.84, noise_prob=0.05,
+                          use_noise=1, t_offset=1)
+        cpu = cpu_baseline(s, args.cpu_traj or 2 * _host_threads(), args.cpu_tf,
+                           _host_threads(), t_offset=1)
+        cpu["unit"] = "periods*trajectories/s"
+    res = {
+        "metric": "Floquet-periods×trajectories/sec of the L=20 real-time adaptive-g loop "
+                  "(controlled-g); RZZ-kernel HBM GB/s vs peak",
+        "value": n_loops * per_loop / elapsed, "unit": "periods*trajectories/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (disorder row 0 of hs/phis_L20.csv)",
+        "config": {"workload": (f"adaptive-g controller (§8(f)2): L={L}, g_initial=0.84, p=0.05, "
+                                f"tf={T}, {shots} trajectories per estimate, exponential "
+                                f"feedback (gain 0.01), one closed loop per step per GPU"),
+                   "L": L, "tf": T, "shots": shots, "parallelism": f"instance-sharded x{world}"},
+        "roofline": roof, "kernels": kern,
+        "ms_per_time_point": elapsed / (args.steps * T) * 1e3,
+        "g_history_mean": (acc[0] / n_loops).tolist(),
+        "device": eng.device_info()["name"],
+    }
+    if cpu:
+        res["cpu_baseline"] = cpu
     print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -337,7 +337,8 @@ dtc::PrepArgs prep_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int
 }
 
 int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* out,
-                       int64_t out_stride) {
+                       int64_t out_stride, int o_first = 0, int n_out = -1,
+                       int accumulate = 0) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->prof) {
     e0 = get_event(ctx);
@@ -345,11 +346,12 @@ int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* 
     DTC_HIP(hipEventRecord(e0, ctx->stream));
   }
   DTC_HIP(dtc::launch_reduce((const double*)ctx->partial.p, n_tiles, n_obs, batch, out,
-                             out_stride, ctx->stream));
+                             out_stride, ctx->stream, o_first, n_out, accumulate));
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     ctx->pending.push_back(
-        Pending{DTC_KERNEL_REDUCE, e0, e1, 8.0 * (double)n_tiles * n_obs * batch});
+        Pending{DTC_KERNEL_REDUCE, e0, e1,
+                8.0 * (double)n_tiles * (n_out < 0 ? n_obs - o_first : n_out) * batch});
   }
   return DTC_OK;
 }
@@ -398,7 +400,7 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
 int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
                      int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
-                     const dtc::KickRec* recs = nullptr) {
+                     const dtc::KickRec* recs = nullptr, int meas_parts = 0) {
   const int shape = pass_shape(ps);
   if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
   const int kind = pass_kind(rc, ps, shape);
@@ -424,6 +426,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.diag_conj = ps.diag == dtc::kDiagConj;
   A.meas = meas_mode;
   A.meas_at_end = meas_at_end;
+  A.meas_parts = meas_parts;
   A.batch = batch;
   A.n_obs = n_obs;
   const int kernel = ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
@@ -438,7 +441,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     ctx->pending.push_back(Pending{kernel, e0, e1, 32.0 * (double)A.state_len * batch});
   }
-  if (meas_mode != dtc::kMeasNone)
+  if (meas_mode != dtc::kMeasNone && meas_out)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
   return DTC_OK;
 }
@@ -1128,74 +1131,102 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
   const Plan& pl = rc.pl;
   const int T = pr->T, L = pr->L;
   const int P = T - 1 + pr->t_offset;
-  const int n_e = 2 * L;   // norm, Z_i, Z_i Z_i+1
-  const int n_x = 1 + L;   // norm, X_i (Z after H)
+  const int n_v = 3 * L;    // per time: norm, Z_i, Z_i Z_i+1, X_i
+  const int n_obs = 4 * L;  // per pass: the above (mid-pass) + X_i before the pre-kick
+  if (n_obs > dtc::kThreads) return fail(DTC_EINVAL, "dtc_energy: L > 64");
   DTC_TRY(upload_tables(ctx, pr, pl));
 
   const int64_t S = (int64_t)pr->n_inst * n_traj;
-  const double per_state = (double)pl.len * 32.0;
+  const double per_state = (double)pl.len * 16.0;
   int64_t B = pr->batch;
   if (B <= 0) {
     size_t free_b = 0, total_b = 0;
     DTC_HIP(hipMemGetInfo(&free_b, &total_b));
-    free_b += ctx->F.n + ctx->E.n;
+    free_b += ctx->F.n;
     const double budget = std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
     B = std::max<int64_t>(1, std::min<int64_t>((int64_t)(budget / per_state), 4096));
   }
   B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
   DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
-  DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));
-  DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * std::max(n_e, n_x) * sizeof(double)));
-  DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_e * sizeof(double)));
-  DTC_TRY(ensure(ctx->vals_e, (size_t)B * T * n_x * sizeof(double)));
+  DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
+  DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_v * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
-  std::vector<double> hv_f((size_t)B * T * n_e), hv_x((size_t)B * T * n_x);
+  std::vector<double> hv_f((size_t)B * T * n_v);
   std::vector<int64_t> masks(B);
+
+  // The schedule: the forward chain one kick layer past the last period
+  // (X_P, no D after it), every pass measuring in flight (meas_parts):
+  //  * a pass closing period p: Z, ZZ after the diagonal and X of its sites
+  //    before their post-kick X_p -> time p - t_offset;
+  //  * a pass whose pre-kick is X_nd (nd diagonals applied): X of its sites
+  //    before that kick -> time nd - t_offset, unless its sites' X at that
+  //    time is already taken (one group: the post-kick of the previous pass).
+  // Each group's X at a time is taken exactly once (checked below); the
+  // reduce accumulates the X ranges into the zeroed per-time rows.
+  struct EPass {
+    PassSpec ps;
+    int parts, t_mid, t_pre;
+  };
+  std::vector<EPass> sched;
+  if (P > 0) {
+    const int G = (int)pl.groups.size();
+    Chain fw = forward_chain(pl, 1, P + 1, dtc::kStreamForward);
+    fw.trailing_d = false;
+    fw.X[P].row = P - 1;  // never observed: any valid table row
+    std::vector<char> x_done((size_t)T * G, 0);
+    while (!fw.done()) {
+      const int nd = fw.nd;
+      EPass e{next_pass(fw), 0, -1, -1};
+      const int g = e.ps.group;
+      if (e.ps.diag != dtc::kDiagNone) {
+        const int t = e.ps.d_index - pr->t_offset;
+        if (t >= 0 && t < T) {
+          e.parts |= dtc::kPartZ;
+          e.t_mid = t;
+          if (e.ps.post.enabled) {
+            e.parts |= dtc::kPartXPost;
+            x_done[(size_t)t * G + g] = 1;
+          }
+        }
+      }
+      const int te = nd - pr->t_offset;
+      if (e.ps.pre.enabled && nd >= 1 && te >= 0 && te < T && !x_done[(size_t)te * G + g]) {
+        e.parts |= dtc::kPartXPre;
+        e.t_pre = te;
+        x_done[(size_t)te * G + g] = 1;
+      }
+      sched.push_back(e);
+    }
+    for (int t = 0; t < T; ++t)
+      for (int g = 0; g < G; ++g)
+        if (t + pr->t_offset >= 1 && !x_done[(size_t)t * G + g])
+          return fail(DTC_EINVAL, "internal: dtc_energy left an X group unmeasured");
+  }
 
   for (int64_t bs = 0; bs < S; bs += B) {
     const int nb = (int)std::min<int64_t>(B, S - bs);
     for (int b = 0; b < nb; ++b)
       masks[b] = (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + (bs + b) % n_traj));
     double2* F = (double2*)ctx->F.p;
-    double2* E = (double2*)ctx->E.p;
+    double* vals = (double*)ctx->vals_f.p;
     DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
                            hipMemcpyHostToDevice, ctx->stream));
     DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
     DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
-    DTC_HIP(hipMemsetAsync(ctx->vals_f.p, 0, (size_t)nb * T * n_e * sizeof(double), ctx->stream));
-    DTC_HIP(hipMemsetAsync(ctx->vals_e.p, 0, (size_t)nb * T * n_x * sizeof(double), ctx->stream));
-    if (P > 0) {
-      Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
-      while (!fw.done()) {
-        PassSpec ps = next_pass(fw);
-        const int p = ps.d_index;
-        const int t = p - pr->t_offset;
-        const bool closes = ps.diag != dtc::kDiagNone;
-        const bool meas = closes && t >= 0;
-        DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, ps, F, F,
-                                 meas ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_e,
-                                 meas ? (double*)ctx->vals_f.p + (size_t)t * n_e : nullptr,
-                                 (int64_t)T * n_e));
-        if (!meas) continue;
-        // X basis: E = H^L . (undo of the kick a group is already ahead by) . F
-        const int G = (int)pl.groups.size();
-        for (int g = 0; g < G; ++g) {
-          PassSpec xs{g, no_kick(), no_kick(), dtc::kDiagNone, 0};
-          xs.pre = fw.kc[g] > p
-                       ? dtc::KickDesc{1, p, dtc::kKickUndoBasisX, dtc::kStreamForward,
-                                       (uint32_t)(p + 1)}
-                       : dtc::KickDesc{1, 0, dtc::kKickBasisX, 0u, 0u};
-          const bool last = g == G - 1;
-          DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, xs, g == 0 ? F : E, E,
-                                   last ? dtc::kMeasSites : dtc::kMeasNone, 1, n_x,
-                                   last ? (double*)ctx->vals_e.p + (size_t)t * n_x : nullptr,
-                                   (int64_t)T * n_x));
-        }
-      }
+    DTC_HIP(hipMemsetAsync(vals, 0, (size_t)nb * T * n_v * sizeof(double), ctx->stream));
+    const int64_t vs = (int64_t)T * n_v;
+    for (const EPass& e : sched) {
+      DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, e.ps, F, F,
+                               e.parts ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_obs, nullptr,
+                               0, nullptr, e.parts));
+      if (e.parts & dtc::kPartZ)
+        DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb, vals + (size_t)e.t_mid * n_v, vs,
+                                   0, 3 * L, 1));
+      if (e.parts & dtc::kPartXPre)
+        DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb,
+                                   vals + (size_t)e.t_pre * n_v + 2 * L, vs, 3 * L, L, 1));
     }
-    DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_e * sizeof(double),
-                           hipMemcpyDeviceToHost, ctx->stream));
-    DTC_HIP(hipMemcpyAsync(hv_x.data(), ctx->vals_e.p, (size_t)nb * T * n_x * sizeof(double),
+    DTC_HIP(hipMemcpyAsync(hv_f.data(), vals, (size_t)nb * T * n_v * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
     DTC_HIP(hipStreamSynchronize(ctx->stream));
     if (ctx->prof) DTC_TRY(resolve_pending(ctx));
@@ -1204,8 +1235,8 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
       const uint64_t m = (uint64_t)masks[b];
       for (int t = 0; t < T; ++t) {
         const bool at_init = (t + pr->t_offset == 0);
-        const double* vf = hv_f.data() + ((size_t)b * T + t) * n_e;
-        const double* vx = hv_x.data() + ((size_t)b * T + t) * n_x;
+        const double* vf = hv_f.data() + ((size_t)b * T + t) * n_v;
+        const double* vx = vf + 2 * L - 1;  // X_i at vx[1 + i]
         double* zo = z + ((size_t)g * T + t) * L;
         double* xo = x + ((size_t)g * T + t) * L;
         for (int i = 0; i < L; ++i) {

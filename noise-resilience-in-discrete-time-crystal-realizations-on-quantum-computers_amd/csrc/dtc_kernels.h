@@ -14,15 +14,30 @@ static constexpr int kThreads = 256;
 static constexpr int kRegs = 16;          // amplitudes per thread (4 register bits)
 static constexpr int kChunkBits = 5;      // diagonal factor tables: 5 sites + next bit
 static constexpr int kMaxChunks = 8;      // L_eff <= 40
-static constexpr int kMaxObs = 64;        // norm + per-site <Z_i> + per-bond <Z_i Z_i+1> (L <= 32)
+// Per-wave reduction slots (s_red): 8 parity vectors x 12 lane patterns for
+// the Z-type observables, then <X> partials of the 12 tile bits at the entry
+// (pre-kick) and mid-pass (post-kick) points of an energy pass.
+static constexpr int kRedLanes = 12;
+static constexpr int kSlotXPre = 8 * kRedLanes;
+static constexpr int kSlotXPost = kSlotXPre + kTileBits;
+static constexpr int kRedSlots = kSlotXPost + kTileBits;
 
 enum DiagMode { kDiagNone = 0, kDiagFwd = 1, kDiagConj = 2 };
 enum MeasMode {
   kMeasNone = 0,
   kMeasProbe = 1,   // (norm, Z_probe)
   kMeasSites = 2,   // (norm, Z_0 .. Z_{L-1})
-  kMeasEnergy = 3,  // (norm, Z_0 .. Z_{L-1}, Z_0 Z_1 .. Z_{L-2} Z_{L-1})
+  kMeasEnergy = 3,  // (norm, Z_i, Z_i Z_i+1, X_i mid-pass, X_i entry): 4 L values
 };
+// Parts of a kMeasEnergy pass (PassArgs::meas_parts).  X_i of a site is the
+// pair product 2 Re sum conj(a_0) a_1 over its register bit, taken in the
+// layout that holds the site in registers just before the site's kick:
+//   kPartZ     norm, Z_i, Z_i Z_i+1 after the diagonal        (obs [0, 2L))
+//   kPartXPost X_i of the kicked sites before the post-kick    (obs [2L, 3L))
+//   kPartXPre  X_i of the kicked sites before the pre-kick     (obs [3L, 4L))
+// Kicks on other sites commute with X_i, so both X points see the state of
+// the time the engine assigns them to (dtc_energy).
+enum MeasPart { kPartZ = 1, kPartXPost = 2, kPartXPre = 4 };
 // Which parts a pass runs: pre-kick (K), diagonal (D), post-kick (K).
 enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4 };
 // Matrix family of every kick in a pass (chosen by the host from the kick
@@ -56,7 +71,8 @@ struct KickDesc {
 // Pauli draws, the sub-gate products and the factored form (SiteMat in
 // dtc_kernels.hip) — instead of once per tile.  Per (pass, state):
 //   rec[k], rec[12 + k]  pre / post kick of tile bit k
-//       RX/RY family: d[0] = coefficient, i[1] = variant;  general: d[0..7] = 2x2
+//       RX/RY family: d[0] = coefficient, i[1] = variant, d[2] = w^2 (the
+//       site's share of the global factor, squared);  general: d[0..7] = 2x2
 //   rec[24]              d[0], d[1] = global factor (i^k * prod of scales),
 //                        d[2] = 1 / w_post^2 (measurement before the post-kick)
 union KickRec {
@@ -129,7 +145,8 @@ struct PassArgs {
   int meas;                // MeasMode
   int probe;
   int meas_at_end;         // measure after the post-kick instead of after the diagonal
-  int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 2 L_real
+  int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 4 L_real
+  int meas_parts;          // kMeasEnergy: MeasPart bits
   double* partial;         // [B][n_tiles][n_obs]
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
@@ -140,9 +157,11 @@ hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
 // act must cover nibble sets {2}, {1,2} or {0,1,2}; L_eff in [12, 32].
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);
 
-// out[b * out_stride + o] = sum over tiles of partial[b][tile][o] (fixed order)
+// out[b * out_stride + o] = sum over tiles of partial[b][tile][o_first + o],
+// o < n_out (fixed order); accumulate: += instead of =
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
-                         double* out, int64_t out_stride, hipStream_t stream);
+                         double* out, int64_t out_stride, hipStream_t stream,
+                         int o_first = 0, int n_out = -1, int accumulate = 0);
 
 // state[b * state_len + idx[b]] = 1 (after the caller zeroed the batch)
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx,

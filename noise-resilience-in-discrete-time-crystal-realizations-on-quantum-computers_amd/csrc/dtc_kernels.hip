@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
       } else {
         r.d[0] = sm.coef;
         r.i[1] = sm.var;
-        for (int e = 2; e < 8; ++e) r.d[e] = 0.0;
+        r.d[2] = sm.scale * sm.scale;
+        for (int e = 3; e < 8; ++e) r.d[e] = 0.0;
       }
       out[half * kTileBits + k] = r;
       ksum += sm.k;
@@ -446,6 +447,17 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
+// Lane patterns kept from a wave's Walsh-Hadamard transform (s_red entries):
+// 0, the single bits 1 .. 32 and the adjacent pairs 3 .. 48 — every site or
+// bond observable needs one of them.  -1: not kept.
+__device__ __forceinline__ int lane_pattern(int m) {
+  if (m == 0) return 0;
+  const int k = __ffs(m) - 1;
+  if (m == (1 << k)) return 1 + k;
+  if (k < 5 && m == (3 << k)) return 7 + k;
+  return -1;
+}
+
 // Per-layout global index of register r: x(r) = x0(t) | off(r), off uniform.
 struct TileMap {
   int64_t tbase;
@@ -493,7 +505,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double2 s_tile[kTile];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
-  __shared__ double s_red[kThreads / 64][kMaxObs];
+  __shared__ double s_red[kThreads / 64][kRedSlots];
 
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;
@@ -596,9 +608,14 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
   };
   // Observables of the tile: (sum |a|^2, sum z_i |a|^2 for the probe or every
-  // site).  Only sites inside the tile need a reduction: a register bit of the
-  // layout from per-thread partial sums, a thread bit from the signed thread
-  // total; a site outside the tile has one sign over the tile (tbase).
+  // site, and in energy mode the bond correlators sum z_i z_i+1 |a|^2).  An
+  // index bit of the tile is a register bit of the layout, a thread bit or
+  // (outside the tile) one sign over the tile (tbase).  Each thread forms
+  // parity vectors over its registers — the total, z of each register bit,
+  // z z of adjacent register bits — and a 6-stage Walsh-Hadamard transform
+  // over the wave leaves, in lane m, the vector's sum signed by the lane-bit
+  // parity m: every observable is one such entry (lane pattern of its thread
+  // bits), summed over the 4 waves with the wave-bit signs.
   auto measure_in = [&](auto lay_tag, double inv_w2) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
@@ -619,13 +636,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       zr[j] = z;
     }
     const bool probe_only = A.meas == kMeasProbe;
+    const bool energy = A.meas == kMeasEnergy;
     auto tile_bit = [&](int site) {
       return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
-    // s_red slots: 0 wave total; probe mode: 1 probe site; site/energy modes:
-    // 1..6 parity sums over lane bits 0..5, 7..10 register-bit site sums,
-    // 11.. bond correlators
-    constexpr int kSlotLane = 1, kSlotReg = 7, kSlotBond = 11;
     if (probe_only) {
       const double tot = wave_sum(ptot);
       if (lane == 0) s_red[wave][0] = tot;
@@ -642,40 +656,35 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         if (lane == 0) s_red[wave][1] = z;
       }
     } else {
-      // every in-tile site at once: a 6-stage Walsh-Hadamard transform of the
-      // lane totals leaves sum_t (-1)^bit_k(t) ptot(t) in lane 2^k and the
-      // wave total in lane 0 (6 shuffles instead of one reduction per site)
-      double h = ptot;
+      double vec[8];
+      vec[0] = ptot;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const double o = __shfl_xor(h, 1 << k, 64);
-        h = ((lane >> k) & 1) ? o - h : h + o;
-      }
-      if (lane == 0) s_red[wave][0] = h;
+      for (int j = 0; j < 4; ++j) vec[1 + j] = zr[j];
+      if (energy) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
-        if (lane == (1 << k)) s_red[wave][kSlotLane + k] = h;
+        for (int j = 0; j < 3; ++j) {
+          double z = 0.0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const double z = wave_sum(zr[j]);
-        if (lane == 0) s_red[wave][kSlotReg + j] = z;
-      }
-    }
-    if (A.meas == kMeasEnergy) {
-      // bond correlators <Z_i Z_i+1>: sign per amplitude, generic reduction
-      for (int i = 0; i + 1 < A.L_real; ++i) {
-        double z = 0.0;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-          const int64_t x = x0 | M.rel(r << (4 * LAY));
-          z += (((x >> i) ^ (x >> (i + 1))) & 1) ? -pr[r] : pr[r];
+          for (int r = 0; r < kRegs; ++r) z += (((r >> j) ^ (r >> (j + 1))) & 1) ? -pr[r] : pr[r];
+          vec[5 + j] = z;
         }
-        z = wave_sum(z);
-        if (lane == 0) s_red[wave][kSlotBond + i] = z;
+      }
+      const int e = lane_pattern(lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j >= 5 && !energy) break;
+        double h = vec[j];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double o = __shfl_xor(h, 1 << k, 64);
+          h = ((lane >> k) & 1) ? o - h : h + o;
+        }
+        if (e >= 0) s_red[wave][j * kRedLanes + e] = h;
       }
     }
     __syncthreads();
-    if (t < A.n_obs) {
+    const int n_mid = probe_only ? 2 : (energy ? 2 * A.L_real : 1 + A.L_real);
+    if (t < n_mid) {
       constexpr int NW = kThreads / 64;
       double acc = 0.0;
       if (probe_only) {
@@ -683,43 +692,99 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
         for (int w = 0; w < NW; ++w) acc += s_red[w][ws];
         if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
-      } else if (t == 0) {
-        for (int w = 0; w < NW; ++w) acc += s_red[w][0];
-      } else if (t <= A.L_real) {
-        const int site = t - 1;
-        const int tb = tile_bit(site);
-        if (tb < 0) {  // one sign over the tile
-          for (int w = 0; w < NW; ++w) acc += s_red[w][0];
-          if ((M.tbase >> site) & 1) acc = -acc;
-        } else if (tb >= 4 * LAY && tb < 4 * LAY + 4) {  // register bit
-          for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotReg + tb - 4 * LAY];
-        } else {  // thread bit q of ybase<LAY>
-          const int q = LAY == 2 ? tb : (LAY == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
-          if (q < 6) {
-            for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotLane + q];
-          } else {  // wave bit
-            for (int w = 0; w < NW; ++w)
-              acc += ((w >> (q - 6)) & 1) ? -s_red[w][0] : s_red[w][0];
+      } else {
+        // observable t: 0 norm, 1..L Z_{t-1}, L+1.. Z_i Z_i+1 (i = t-1-L)
+        const int i0 = t <= A.L_real ? t - 1 : t - 1 - A.L_real;
+        const int ns = t == 0 ? 0 : (t <= A.L_real ? 1 : 2);
+        int regs = 0, lanes = 0, waves = 0, neg = 0;
+        for (int k = 0; k < ns; ++k) {
+          const int site = i0 + k;
+          const int tb = tile_bit(site);
+          if (tb < 0) {
+            neg ^= (int)((M.tbase >> site) & 1);
+          } else if (tb >= 4 * LAY && tb < 4 * LAY + 4) {
+            regs |= 1 << (tb - 4 * LAY);
+          } else {
+            const int q = LAY == 2 ? tb : (LAY == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
+            if (q < 6) lanes |= 1 << q;
+            else waves |= 1 << (q - 6);
           }
         }
-      } else {
-        for (int w = 0; w < NW; ++w) acc += s_red[w][kSlotBond + t - 1 - A.L_real];
+        // registers: none -> total, one bit j -> z_j, adjacent bits j, j+1 -> zz_j
+        const int vi = regs == 0 ? 0 : (__popc(regs) == 1 ? 1 + __ffs(regs) - 1 : 5 + __ffs(regs) - 1);
+        const int slot = vi * kRedLanes + max(0, lane_pattern(lanes));
+        for (int w = 0; w < NW; ++w) acc += (__popc(w & waves) & 1) ? -s_red[w][slot] : s_red[w][slot];
+        if (neg) acc = -acc;
       }
       acc *= inv_w2;
       A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
     }
   };
+  // <X> partials of the 4 sites in register nibble LAY (energy mode): lanes
+  // 0, 16, 32, 48 of each wave end with the wave sums of register bits 0..3
+  // (2 + 1 shuffles halve the 4 values over lane bits 5, 4; 4 more finish).
+  auto measure_x = [&](auto lay_tag, double scale, int slot0) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int wave = t >> 6, lane = t & 63;
+    double a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double x = 0.0;
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        if (r & (1 << q)) continue;
+        const double2 u = v[r], w = v[r | (1 << q)];
+        x = fma(u.x, w.x, fma(u.y, w.y, x));
+      }
+      a[q] = x;
+    }
+    const bool h5 = lane & 32, h4 = lane & 16;
+    double k0 = h5 ? a[2] : a[0], k1 = h5 ? a[3] : a[1];
+    const double s0 = h5 ? a[0] : a[2], s1 = h5 ? a[1] : a[3];
+    k0 += __shfl_xor(s0, 32, 64);
+    k1 += __shfl_xor(s1, 32, 64);
+    double k = h4 ? k1 : k0;
+    k += __shfl_xor(h4 ? k0 : k1, 16, 64);
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) k += __shfl_xor(k, off, 64);
+    if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = 2.0 * scale * k;
+  };
+  // squared share of the global factor carried by the factored kicks of
+  // nibble N (records rec0 + 4N .. +3): measuring after them multiplies sums by
+  // the inverse, see the scale bookkeeping at the X points below
+  auto nib_w2 = [&](int N, int rec0) {
+    if (KIND != kKindRX && KIND != kKindRY) return 1.0;
+    double w2 = 1.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w2 *= R.d(rec0 + 4 * N + q, 2);
+    return w2;
+  };
+  const bool x_pre = A.meas == kMeasEnergy && (A.meas_parts & kPartXPre);
+  const bool x_post = A.meas == kMeasEnergy && (A.meas_parts & kPartXPost);
   using IC2 = std::integral_constant<int, 2>;
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
+  // (X before a nibble's pre-kick: the state is exact times the factored
+  // kicks already applied, whose squared scale is 1 / prod w^2)
+  using L0 = std::integral_constant<int, 0>;
+  using L1 = std::integral_constant<int, 1>;
+  using L2 = std::integral_constant<int, 2>;
   if constexpr (RP::pre) {
-    if constexpr (RP::n2) apply_nibble<2, KIND>(v, R, 0);
+    double sc = 1.0;
+    if constexpr (RP::n2) {
+      if (x_pre) measure_x(L2{}, sc, kSlotXPre);
+      apply_nibble<2, KIND>(v, R, 0);
+      if (x_pre) sc *= nib_w2(2, 0);
+    }
     if constexpr (RP::n0) {
       exchange<2, 0>(v, s_tile, t);
+      if (x_pre) measure_x(L0{}, sc, kSlotXPre);
       apply_nibble<0, KIND>(v, R, 0);
+      if (x_pre) sc *= nib_w2(0, 0);
     }
     if constexpr (RP::n1) {
       exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
+      if (x_pre) measure_x(L1{}, sc, kSlotXPre);
       apply_nibble<1, KIND>(v, R, 0);
     }
   }
@@ -733,20 +798,30 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // ---- diagonal and measurement at d_lay ----
   using DL = std::integral_constant<int, RP::d_lay>;
   if constexpr (RP::diag) diag_in(DL{});
-  if (A.meas != kMeasNone && !A.meas_at_end) measure_in(DL{}, inv_w2_mid);  // before the post-kick
+  if (A.meas != kMeasNone && !A.meas_at_end &&
+      (A.meas != kMeasEnergy || (A.meas_parts & kPartZ)))
+    measure_in(DL{}, inv_w2_mid);  // before the post-kick
   DTC_TS(4);
   // ---- post-kick rounds: 1 -> 0 -> 2 ----
+  // (X before a nibble's post-kick: scale 1 / w_post^2 times prod w^2 of the
+  // post nibbles already applied)
   if constexpr (RP::post) {
+    double sc = inv_w2_mid;
     if constexpr (RP::n1) {
       exchange<RP::d_lay, 1>(v, s_tile, t);
+      if (x_post) measure_x(L1{}, sc, kSlotXPost);
       apply_nibble<1, KIND>(v, R, kTileBits);
+      if (x_post) sc *= nib_w2(1, kTileBits);
     }
     if constexpr (RP::n0) {
       exchange<RP::p1, 0>(v, s_tile, t);
+      if (x_post) measure_x(L0{}, sc, kSlotXPost);
       apply_nibble<0, KIND>(v, R, kTileBits);
+      if (x_post) sc *= nib_w2(0, kTileBits);
     }
     if constexpr (RP::n2) {
       exchange<RP::p0, 2>(v, s_tile, t);
+      if (x_post) measure_x(L2{}, sc, kSlotXPost);
       apply_nibble<2, KIND>(v, R, kTileBits);
     }
     exchange<RP::p2, 2>(v, s_tile, t);
@@ -754,6 +829,23 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     exchange<RP::d_lay, 2>(v, s_tile, t);
   }
   if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{}, 1.0);
+  if (x_pre || x_post) {
+    // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
+    // (0 for sites this pass does not kick)
+    __syncthreads();
+    const int L = A.L_real;
+    if (t >= 2 * L && t < 4 * L) {
+      const bool pre = t >= 3 * L;
+      const int site = pre ? t - 3 * L : t - 2 * L;
+      const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+      double acc = 0.0;
+      if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
+        const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
+        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
+      }
+      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    }
+  }
   DTC_TS(5);
 
   char* dst = (char*)(A.dst + b * A.state_len);
@@ -836,15 +928,16 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
 // (state, 8 observables), fixed summation order (strided per thread, then an
 // LDS tree), so results do not depend on the batch a state ran in.
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partial,
-                                                     int n_tiles, int n_obs, int batch,
+                                                     int n_tiles, int n_obs, int o_first,
+                                                     int n_out, int accumulate,
                                                      double* __restrict__ out,
                                                      int64_t out_stride) {
   __shared__ double s_acc[8][256];
   const int b = blockIdx.y, o0 = blockIdx.x * 8, t = threadIdx.x;
-  const int no = min(8, n_obs - o0);
+  const int no = min(8, n_out - o0);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int k = t; k < n_tiles; k += 256) {
-    const double* p = partial + ((int64_t)b * n_tiles + k) * n_obs + o0;
+    const double* p = partial + ((int64_t)b * n_tiles + k) * n_obs + o_first + o0;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (j < no) acc[j] += p[j];
@@ -859,13 +952,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
     }
     __syncthreads();
   }
-  if (t < no) out[(int64_t)b * out_stride + o0 + t] = s_acc[t][0];
+  if (t < no) {
+    double* o = out + (int64_t)b * out_stride + o0 + t;
+    *o = accumulate ? *o + s_acc[t][0] : s_acc[t][0];
+  }
 }
 
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
-                         double* out, int64_t out_stride, hipStream_t stream) {
-  hipLaunchKernelGGL(reduce_kernel, dim3((n_obs + 7) / 8, batch), dim3(256), 0, stream, partial,
-                     n_tiles, n_obs, batch, out, out_stride);
+                         double* out, int64_t out_stride, hipStream_t stream, int o_first,
+                         int n_out, int accumulate) {
+  if (n_out < 0) n_out = n_obs - o_first;
+  if (o_first < 0 || n_out < 1 || o_first + n_out > n_obs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(reduce_kernel, dim3((n_out + 7) / 8, batch), dim3(256), 0, stream, partial,
+                     n_tiles, n_obs, o_first, n_out, accumulate, out, out_stride);
   return hipGetLastError();
 }
 

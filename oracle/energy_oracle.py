@@ -28,15 +28,17 @@ def prep_mask(spec, seed, traj):
 
 
 def observables(psi, L):
-    N = 1 << L
-    x = np.arange(N)
+    """<Z_i>, <Z_i Z_i+1>, <X_i> of a state vector (one site at a time, so
+    L=24 stays within a few hundred MB)."""
+    x = np.arange(1 << L, dtype=np.int64)
     pr = np.abs(psi) ** 2
-    zb = 1 - 2 * ((x[None, :] >> np.arange(L)[:, None]) & 1)
-    z = zb @ pr
-    zz = np.array([(zb[i] * zb[i + 1]) @ pr for i in range(L - 1)])
-    xs = np.array([2.0 * np.real(np.conj(psi[x[((x >> i) & 1) == 0]])
-                                 * psi[x[((x >> i) & 1) == 0] ^ (1 << i)]).sum()
-                   for i in range(L)])
+    zsign = [1.0 - 2.0 * ((x >> i) & 1) for i in range(L)]
+    z = np.array([zb @ pr for zb in zsign])
+    zz = np.array([(zsign[i] * zsign[i + 1]) @ pr for i in range(L - 1)])
+    xs = np.empty(L)
+    for i in range(L):
+        lo = x[((x >> i) & 1) == 0]
+        xs[i] = 2.0 * np.real(np.conj(psi[lo]) * psi[lo ^ (1 << i)]).sum()
     return z, zz, xs
 
 

@@ -32,6 +32,36 @@ def test_energy_matches_oracle(pkg, engine, L, T, p, state, pol):
             assert np.abs(got["x"][inst, tr] - x).max() < TOL
 
 
+@pytest.mark.parametrize("L,state,pol", [(20, "neel", "x"), (24, "vacuum", "y")])
+def test_energy_large_matches_oracle(pkg, engine, L, state, pol):
+    """Two site groups (L=20: sites 0-11 | 12-19) and three (L=24): every
+    group's <X_i> comes from a different pass (mid-pass or next-pass entry)."""
+    rng = np.random.default_rng(L + 7)
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=3, hs=hs, phis=phis, g=0.93, noise_prob=0.05, polarization=pol,
+                         initial_state=state)
+    got = engine.energy(spec, 2, seed=5)
+    for tr in range(2):
+        z, zz, x = energy_oracle.trajectory_energy(spec, 0, tr, seed=5)
+        assert np.abs(got["z"][0, tr] - z).max() < TOL
+        assert np.abs(got["zz"][0, tr] - zz).max() < TOL
+        assert np.abs(got["x"][0, tr] - x).max() < TOL
+
+
+def test_energy_t_offset_and_batches(pkg, engine):
+    """t_offset=1 (first row after one period) and a batch split: the same
+    per-trajectory values as one batch from t_offset 0 shifted by one."""
+    rng = np.random.default_rng(3)
+    L = 13
+    hs, phis = random_disorder(rng, L)
+    base = pkg.SweepSpec(L=L, T=5, hs=hs, phis=phis, g=0.95, noise_prob=0.05)
+    off = pkg.SweepSpec(L=L, T=4, hs=hs, phis=phis, g=0.95, noise_prob=0.05, t_offset=1)
+    a = engine.energy(base, 5, seed=9)
+    b = engine.energy(off, 5, seed=9, batch=2)
+    for k in ("z", "zz", "x"):
+        assert np.abs(a[k][:, :, 1:] - b[k]).max() < TOL, k
+
+
 def test_energy_mean_vs_density_matrix(pkg, engine):
     rng = np.random.default_rng(8)
     L, T, p, n = 4, 10, 0.1, 4096
