@@ -83,10 +83,10 @@ def cpu_baseline(spec, n_traj, T_sample, threads, t_offset=0):
     }
 
 
-def read_traffic(bytes_per_launch):
-    """HBM bytes per launch of the RZZ kernel from the committed PMC summary
-    (tools/pmc_summary.py output), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+def read_traffic(bytes_per_launch, suffix="_pmc.json"):
+    """HBM bytes per launch of the RZZ kernel from the latest committed PMC
+    summary named *<suffix> (tools/pmc_summary.py output), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -587,11 +587,14 @@ def main_energy(args):
     mean = {"z": acc[0] / n, "zz": acc[1, :, :L - 1] / n, "x": acc[2] / n}
     e_t = pkg.energy.energy_from_observables(mean, L, 0.97, hs[0], phis[0], "full") / L
     roof, kern = _pass_kernels(stats, elapsed)
-    roof["kernel"] = "dtc_kdk_pass (forward period, Z/ZZ reduction fused in the epilogue)"
+    roof["kernel"] = ("dtc_kdk_pass (one forward period; Z, ZZ after the diagonal and X before "
+                      "each site's kick measured in flight)")
+    roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"],
+                                                           "_pmc_energy.json")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_energy(spec, args.cpu_traj or _host_threads(),
-                                  min(args.cpu_tf, 4), _host_threads())
+        cpu = cpu_baseline_energy(spec, args.cpu_traj or 2 * _host_threads(),
+                                  min(args.cpu_tf, 6), _host_threads())
     res = {
         "metric": "Floquet-periods×trajectories/sec at L=20 with <Z_i>,<Z_iZ_i+1>,<X_i> per "
                   "period (energy path); RZZ-kernel HBM GB/s vs peak",
@@ -664,6 +667,8 @@ def main_ctrl(args):
     per_loop = shots * sum(2 * (t + 1) for t in range(T))
     n_loops = world * args.steps
     roof, kern = _pass_kernels(stats, elapsed)
+    # the same kernel (probe measurement) as C2: its PMC ratio, scaled
+    roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"])
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         hs_, phis_ = load_disorder_row(L)
