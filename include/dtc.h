@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 3
+#define DTC_ABI_VERSION 4
 
 /* error codes */
 #define DTC_OK 0
@@ -207,6 +207,16 @@ int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups);
  * (energy.py:83-102 builds its labels big-endian, see energy.py here). */
 int dtc_energy(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise, uint64_t seed,
                int64_t traj_offset, int32_t n_traj, double* z, double* zz, double* x);
+
+/* dtc_energy under device-like noise (the FakeBrisbane estimator runs of
+ * autocorr-delta-a-single-qiskit-fast-energy-fakebrisbane.py:131-192, with a
+ * user-supplied calibration, see dtc_device_noise).  Same outputs, as the
+ * Kraus-weighted (unnormalised) expectations of each trajectory: their mean is
+ * the channel's expectation.  Read-out error is NOT applied here (anc_factor
+ * and readout_p01/p10 are ignored); the caller maps the means (energy.py). */
+int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_noise* dv,
+                      uint64_t seed, int64_t traj_offset, int32_t n_traj, double* z, double* zz,
+                      double* x);
 
 /* Profiling: when enabled, every kernel launch is bracketed by HIP events on
  * the ctx stream and accumulated per kernel kind. */

@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "dtc_plan_groups",
     "dtc_energy",
     "dtc_autocorr_device",
+    "dtc_energy_device",
 )
 
 KERNEL_LO_PASS = 0
@@ -162,6 +163,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_int32, _dp, _dp, _dp,
         ]
         lib.dtc_autocorr_device.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcDeviceNoise), ctypes.c_uint64, ctypes.c_int64,
+            ctypes.c_int32, _dp, _dp, _dp,
+        ]
+        lib.dtc_energy_device.argtypes = [
             ctypes.c_void_p, P(DtcProblem), P(DtcDeviceNoise), ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_int32, _dp, _dp, _dp,
         ]

@@ -1111,8 +1111,11 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
 }
 
 
-int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,
-               int64_t traj_offset, int32_t n_traj, double* z, double* zz, double* x) {
+namespace {
+
+int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset, int32_t n_traj,
+                double* z, double* zz, double* x) {
   if (!ctx || !z || !x || (!zz && pr && pr->L > 1)) return fail(DTC_EINVAL, "null ctx/outputs");
   DTC_TRY(check_problem(pr, nz));
   if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
@@ -1128,6 +1131,7 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
   rc.noisy = nz->p > 0.0 ? 1 : 0;
   rc.row_kind = classify_rows(pr);
   thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  if (dv) DTC_TRY(setup_device_noise(ctx, pr, dv, rc));
   const Plan& pl = rc.pl;
   const int T = pr->T, L = pr->L;
   const int P = T - 1 + pr->t_offset;
@@ -1142,12 +1146,14 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
   if (B <= 0) {
     size_t free_b = 0, total_b = 0;
     DTC_HIP(hipMemGetInfo(&free_b, &total_b));
-    free_b += ctx->F.n;
+    free_b += ctx->F.n + (dv ? ctx->E.n : 0);
     const double budget = std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
-    B = std::max<int64_t>(1, std::min<int64_t>((int64_t)(budget / per_state), 4096));
+    B = std::max<int64_t>(1, std::min<int64_t>((int64_t)(budget / (dv ? 2 * per_state : per_state)),
+                                               4096));
   }
   B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
   DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
+  if (dv) DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_v * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
@@ -1163,12 +1169,34 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
   //    time is already taken (one group: the post-kick of the previous pass).
   // Each group's X at a time is taken exactly once (checked below); the
   // reduce accumulates the X ranges into the zeroed per-time rows.
+  //
+  // Device-like noise: a non-unitary kick on one site changes <X> of the
+  // others, so nothing is measured across a kick.  The chain starts no layer
+  // in a pass that applies D (2 passes per period); after the pass closing
+  // period p the state is exactly the state at p: Z, ZZ mid-pass, then X by
+  // one noiseless basis-change pass per site group (E = H^L F).
   struct EPass {
     PassSpec ps;
     int parts, t_mid, t_pre;
+    bool xbasis;
   };
   std::vector<EPass> sched;
-  if (P > 0) {
+  if (P > 0 && dv) {
+    Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
+    fw.post_after_d = false;
+    while (!fw.done()) {
+      EPass e{next_pass(fw), 0, -1, -1, false};
+      if (e.ps.diag != dtc::kDiagNone) {
+        const int t = e.ps.d_index - pr->t_offset;
+        if (t >= 0 && t < T) {
+          e.parts = dtc::kPartZ;
+          e.t_mid = t;
+          e.xbasis = true;
+        }
+      }
+      sched.push_back(e);
+    }
+  } else if (P > 0) {
     const int G = (int)pl.groups.size();
     Chain fw = forward_chain(pl, 1, P + 1, dtc::kStreamForward);
     fw.trailing_d = false;
@@ -1176,7 +1204,7 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
     std::vector<char> x_done((size_t)T * G, 0);
     while (!fw.done()) {
       const int nd = fw.nd;
-      EPass e{next_pass(fw), 0, -1, -1};
+      EPass e{next_pass(fw), 0, -1, -1, false};
       const int g = e.ps.group;
       if (e.ps.diag != dtc::kDiagNone) {
         const int t = e.ps.d_index - pr->t_offset;
@@ -1221,10 +1249,23 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
                                0, nullptr, e.parts));
       if (e.parts & dtc::kPartZ)
         DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb, vals + (size_t)e.t_mid * n_v, vs,
-                                   0, 3 * L, 1));
+                                   0, (e.parts & dtc::kPartXPost) ? 3 * L : 2 * L, 1));
       if (e.parts & dtc::kPartXPre)
         DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb,
                                    vals + (size_t)e.t_pre * n_v + 2 * L, vs, 3 * L, L, 1));
+      if (e.xbasis) {
+        double2* E = (double2*)ctx->E.p;
+        const int G = (int)pl.groups.size();
+        for (int g = 0; g < G; ++g) {
+          PassSpec xs{g, no_kick(), no_kick(), dtc::kDiagNone, 0};
+          xs.pre = dtc::KickDesc{1, 0, dtc::kKickBasisX, 0u, 0u, 0u};
+          const bool last = g == G - 1;
+          DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, xs, g == 0 ? F : E, E,
+                                   last ? dtc::kMeasSites : dtc::kMeasNone, 1, 1 + L, nullptr, 0));
+        }
+        DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, 1 + L, nb,
+                                   vals + (size_t)e.t_mid * n_v + 2 * L, vs, 1, L, 1));
+      }
     }
     DTC_HIP(hipMemcpyAsync(hv_f.data(), vals, (size_t)nb * T * n_v * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
@@ -1253,6 +1294,21 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_
     }
   }
   return DTC_OK;
+}
+
+}  // namespace
+
+int dtc_energy(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,
+               int64_t traj_offset, int32_t n_traj, double* z, double* zz, double* x) {
+  return energy_impl(ctx, pr, nz, nullptr, seed, traj_offset, n_traj, z, zz, x);
+}
+
+int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_noise* dv,
+                      uint64_t seed, int64_t traj_offset, int32_t n_traj, double* z, double* zz,
+                      double* x) {
+  if (!dv) return fail(DTC_EINVAL, "null device noise");
+  const dtc_noise nz{0.0, 0, 0};
+  return energy_impl(ctx, pr, &nz, dv, seed, traj_offset, n_traj, z, zz, x);
 }
 
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups) {

@@ -111,6 +111,16 @@ class DeviceCalibration:
                    sx_gate_ns=float(d["sx_gate_ns"]), kick_sx_count=int(d.get("kick_sx_count", 2)),
                    cz_error=float(d.get("cz_error", 0.0)), note=d.get("note", ""))
 
+    def site_readout(self, L: int):
+        """Per-site read-out flip probabilities (p01[L], p10[L]) of the chain
+        qubits (qubits[1..L]): the energy estimator measures every site."""
+        if len(self.qubits) < L + 1:
+            raise ValueError(f"calibration {self.name!r} has {len(self.qubits)} qubits, "
+                             f"need {L + 1} (ancilla + {L} sites)")
+        sites = self.qubits[1:L + 1]
+        return (np.array([float(q.get("readout_p01", 0.0)) for q in sites]),
+                np.array([float(q.get("readout_p10", 0.0)) for q in sites]))
+
     def device_noise(self, L: int, n_anc_1q: int = 6, n_anc_2q: int = 2) -> DeviceNoise:
         """Channel parameters for an L-site chain (qubits[1..L]) with the
         ancilla on qubits[0].  A kick = ``kick_sx_count`` sx pulses: error

@@ -111,13 +111,35 @@ def _engine(engine):
     return sweep._default_engine()
 
 
+def readout_observables(obs: dict, p01, p10) -> dict:
+    """Per-site read-out error on measured expectations: a bit reads 1 for 0
+    w.p. p01[i] and 0 for 1 w.p. p10[i], independently, so a measured z_i is
+    a_i z_i + b_i in expectation (a = 1 - p01 - p10, b = p10 - p01) and
+    z_i z_i+1 -> a_i a_i+1 zz + a_i b_i+1 z_i + b_i a_i+1 z_i+1 + b_i b_i+1.
+    X_i is measured after the estimator's basis change: a_i x_i + b_i."""
+    p01 = np.asarray(p01, dtype=float)
+    p10 = np.asarray(p10, dtype=float)
+    a, b = 1.0 - p01 - p10, p10 - p01
+    z, zz, x = obs["z"], obs["zz"], obs["x"]
+    out = {"z": a * z + b, "x": a * x + b}
+    if z.shape[-1] > 1:
+        out["zz"] = (a[:-1] * a[1:] * zz + a[:-1] * b[1:] * z[..., :-1]
+                     + b[:-1] * a[1:] * z[..., 1:] + b[:-1] * b[1:])
+    else:
+        out["zz"] = zz
+    return out
+
+
 def get_instances_energy(spec: SweepSpec, n_traj: int = ESTIMATOR_SHOTS,
                          hamiltonian_types=("full",), seed: int = 0x5EED0001, engine=None,
-                         traj_offset: int = 0) -> dict:
+                         traj_offset: int = 0, readout=None) -> dict:
     """``get_instances`` of the energy scripts: ``<H>(t)`` per instance
     (``[inst][T]``) for each requested Hamiltonian variant, as the trajectory
-    mean of the engine's per-trajectory observables."""
+    mean of the engine's per-trajectory observables (``readout`` = per-site
+    (p01, p10) applied to them, device-like noise)."""
     obs = _engine(engine).energy(spec, n_traj, seed=seed, traj_offset=traj_offset)
+    if readout is not None:
+        obs = readout_observables(obs, *readout)
     out = {}
     for ht in hamiltonian_types:
         per = np.stack([
@@ -159,6 +181,21 @@ def run_energy(L, g, hs, phis, T, nprobs=(0, 0.001, 0.01, 0.1), use_noise=1,
         for ht, v in per.items():
             res[(ht, nprob)] = v.mean(axis=0) / L
     return res
+
+
+def run_energy_device(L, g, hs, phis, T, calibration, initial_state="vacuum",
+                      n_traj=ESTIMATOR_SHOTS, seed=0x5EED0001, engine=None):
+    """energy-fakebrisbane.py's main loop (:226-234): ``<H>(t)`` under the
+    device's noise (here: device-like noise from a calibration file, see
+    device_noise.py; FakeBrisbane's own data is unavailable offline), read-out
+    error on every measured site, mean over instances — NOT divided by L (the
+    script saves ``np.mean(energy, axis=0)`` as is)."""
+    spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
+                     noise_prob=0.0, use_noise=1)
+    spec.device = calibration.device_noise(L)
+    per = get_instances_energy(spec, n_traj, ("full",), seed, engine,
+                               readout=calibration.site_readout(L))["full"]
+    return per.mean(axis=0)
 
 
 def write_energy_csv(path: str, ts, columns: dict) -> str:

@@ -10,8 +10,14 @@
 
 Flags as energy.py:26-40; files and folders as the scripts write them
 (energy.py:57-61, 229-234; ham-comparison.py:277-280; vs-echo.py:248-251).
-Values are ``mean over instances of <H>(t) / L``.  ``--use_fakebackend 1``
-needs FakeBrisbane calibration data, which is not available offline: error.
+Values are ``mean over instances of <H>(t) / L``.
+
+    --use_fakebackend 1    ...-energy-fakebrisbane.py: device-like noise from
+                           --device_calibration (FakeBrisbane's own snapshot is not
+                           available offline; default: the documented stand-in
+                           data/device_standin_L20.json), per-site read-out error;
+                           column energy_p_fakebrisbane = mean over instances of
+                           <H>(t) (not divided by L, as that script saves it)
 """
 from __future__ import annotations
 
@@ -39,6 +45,8 @@ def build_parser():
     p.add_argument("--use_noise", type=int, default=1)
     p.add_argument("--initial_state", type=str, default="vacuum", choices=["vacuum", "neel"])
     p.add_argument("--use_fakebackend", type=int, default=0)
+    p.add_argument("--device_calibration", type=str, default=None,
+                   help="calibration JSON for --use_fakebackend 1 (default: the stand-in)")
     p.add_argument("--trajectories", type=int, default=en.ESTIMATOR_SHOTS,
                    help="trajectories per point (default: the estimator's 4096 shots)")
     p.add_argument("--seed", type=int, default=0x5EED0001)
@@ -49,15 +57,24 @@ def build_parser():
 
 def main(argv=None):
     args = build_parser().parse_args(argv)
-    if args.use_fakebackend:
-        raise SystemExit("use_fakebackend=1: FakeBrisbane calibration data is not available "
-                         "offline (qiskit-ibm-runtime); see DESIGN.md")
     L, T = args.L, args.tf
     hs, phis = load_disorder(L, args.inst, args.disorder_folder)
     ts = np.arange(0, T)
     name_args = (args.initial_state, args.g, L, args.inst, args.randomphi, args.phi_delta,
                  args.phi_amplitude, args.noise_prob, args.use_noise)
-    if args.mode == "full":
+    if args.use_fakebackend:
+        from .cli import DEFAULT_CALIBRATION
+        from .device_noise import DeviceCalibration
+
+        cal_path = args.device_calibration or DEFAULT_CALIBRATION
+        cal = DeviceCalibration.from_json(cal_path)
+        print(f"Device-like noise from {cal_path} ({cal.name})")
+        e = en.run_energy_device(L, args.g, hs, phis, T, cal, initial_state=args.initial_state,
+                                 n_traj=args.trajectories, seed=args.seed)
+        cols = {"energy_p_fakebrisbane": e}
+        path = os.path.join(args.out_dir, en.energy_folder(L, "fakebrisbane"),
+                            en.energy_csv_name("energy_data", *name_args))
+    elif args.mode == "full":
         nprobs = [0, 0.001, 0.01, 0.1]
         noisy = bool(args.use_noise)
         res = en.run_energy(L, args.g, hs, phis, T, nprobs, use_noise=int(noisy),

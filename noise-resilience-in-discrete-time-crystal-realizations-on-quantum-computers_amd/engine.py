@@ -201,17 +201,28 @@ class DtcEngine:
 
     def energy(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
                traj_offset: int = 0, batch: int = 0):
-        """Per-trajectory energy observables of the forward sweep (dtc_energy):
-        ``z`` [n_inst][n_traj][T][L], ``zz`` [..][L-1], ``x`` [..][L]."""
+        """Per-trajectory energy observables of the forward sweep (dtc_energy,
+        or dtc_energy_device when ``spec.device`` is set: Kraus-weighted
+        expectations, read-out error not applied): ``z`` [n_inst][n_traj][T][L],
+        ``zz`` [..][L-1], ``x`` [..][L]."""
         n_inst, T, L = spec.n_inst, spec.T, spec.L
         z = np.zeros((n_inst, n_traj, T, L))
         zz = np.zeros((n_inst, n_traj, T, max(L - 1, 0)))
         x = np.zeros((n_inst, n_traj, T, L))
         pr = self._problem(spec, True, False, batch, 0)
-        _capi.check(self._lib.dtc_energy(
-            self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)), ctypes.c_uint64(seed),
-            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(z),
-            _capi.as_dptr(zz) if L > 1 else None, _capi.as_dptr(x)))
+        outs = (_capi.as_dptr(z), _capi.as_dptr(zz) if L > 1 else None, _capi.as_dptr(x))
+        if spec.device is not None:
+            if spec.device.L != spec.L:
+                raise ValueError("device noise has a different number of sites")
+            dv = _capi.device_struct(spec.device)
+            _capi.check(self._lib.dtc_energy_device(
+                self._ctx, ctypes.byref(pr), ctypes.byref(dv), ctypes.c_uint64(seed),
+                ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), *outs))
+        else:
+            _capi.check(self._lib.dtc_energy(
+                self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)),
+                ctypes.c_uint64(seed), ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj),
+                *outs))
         return {"z": z, "zz": zz, "x": x}
 
     # -- sharded state (dtc_shard_*; driver: sharded.py) ----------------

@@ -61,6 +61,14 @@ def lib():
         _lib.orc_autocorr_device.argtypes = [
             ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcDeviceNoise), ctypes.c_uint64,
             ctypes.c_int64, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]
+        _lib.orc_apply_periods_device.argtypes = [
+            ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcDeviceNoise), ctypes.c_uint64,
+            ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_int32, _dp, _dp]
+        _lib.orc_init_mask.argtypes = [ctypes.POINTER(OrcProblem), ctypes.c_double,
+                                       ctypes.POINTER(OrcDeviceNoise), ctypes.c_uint64,
+                                       ctypes.c_int64]
+        _lib.orc_init_mask.restype = ctypes.c_int64
     return _lib
 
 
@@ -86,6 +94,18 @@ def _noise(spec, n_anc=6):
     return nz
 
 
+def _device(spec):
+    """OrcDeviceNoise of spec.device (its arrays stay owned by spec.device), or None."""
+    dev = getattr(spec, "device", None)
+    if dev is None:
+        return None
+    dv = OrcDeviceNoise()
+    dv.p_gate, dv.t1_us, dv.t2_us = _ptr(dev.p_gate), _ptr(dev.t1_us), _ptr(dev.t2_us)
+    dv.gate_ns, dv.anc_factor = dev.gate_ns, dev.anc_factor
+    dv.readout_p01, dv.readout_p10 = dev.readout_p01, dev.readout_p10
+    return dv
+
+
 def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_echo=True,
              want_zsite=False, n_threads=0, t_first=0):
     """Same contract as DtcEngine.autocorr (per-trajectory outputs)."""
@@ -93,12 +113,8 @@ def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_e
     fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
     echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
     zs = np.zeros((n_inst, n_traj, T, L)) if want_zsite else None
-    dev = getattr(spec, "device", None)
-    if dev is not None:
-        dv = OrcDeviceNoise()
-        dv.p_gate, dv.t1_us, dv.t2_us = _ptr(dev.p_gate), _ptr(dev.t1_us), _ptr(dev.t2_us)
-        dv.gate_ns, dv.anc_factor = dev.gate_ns, dev.anc_factor
-        dv.readout_p01, dv.readout_p10 = dev.readout_p01, dev.readout_p10
+    dv = _device(spec)
+    if dv is not None:
         rc = lib().orc_autocorr_device(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
                                        ctypes.byref(dv), seed, traj_offset, n_traj, _ptr(fwd),
                                        _ptr(echo), _ptr(zs), n_threads)
@@ -122,10 +138,28 @@ def apply_periods(spec, state, first_period, n_periods, inverse=False, inst=0, t
                   stream=0, seed=0x5EED0001):
     psi = np.ascontiguousarray(state, dtype=np.complex128).copy()
     z = np.zeros(1 + spec.L)
-    lib().orc_apply_periods(ctypes.byref(_problem(spec)), ctypes.byref(_noise(spec)), seed, inst,
-                            traj, stream, first_period, n_periods, int(inverse),
-                            _ptr(psi.view(np.float64)), _ptr(z))
+    dv = _device(spec)
+    if dv is not None:
+        rc = lib().orc_apply_periods_device(ctypes.byref(_problem(spec)), ctypes.byref(dv), seed,
+                                            inst, traj, stream, first_period, n_periods,
+                                            int(inverse), _ptr(psi.view(np.float64)), _ptr(z))
+    else:
+        rc = lib().orc_apply_periods(ctypes.byref(_problem(spec)), ctypes.byref(_noise(spec)),
+                                     seed, inst, traj, stream, first_period, n_periods,
+                                     int(inverse), _ptr(psi.view(np.float64)), _ptr(z))
+    if rc != 0:
+        raise RuntimeError(f"orc_apply_periods failed: {rc}")
     return psi, z
+
+
+def init_mask(spec, seed, traj):
+    """Basis state after the noisy neel preparation (depolarizing or device)."""
+    dv = _device(spec)
+    m = lib().orc_init_mask(ctypes.byref(_problem(spec)), spec.p,
+                            ctypes.byref(dv) if dv is not None else None, seed, traj)
+    if m < 0:
+        raise RuntimeError(f"orc_init_mask failed: {m}")
+    return int(m)
 
 
 def sample_pauli(p, seed, traj, stream, period, site, sub):

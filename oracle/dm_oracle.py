@@ -321,17 +321,21 @@ def statevector_zsite(L, T, hs, phis, kick, init_mask=0, t_offset=0):
     return out
 
 
-def energy_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", t_offset=0):
+def energy_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", t_offset=0, dev=None):
     """Exact <Z_i>, <Z_i Z_i+1>, <X_i> of the L-qubit energy circuit
     (autocorr-delta-a-single-qiskit-fast-energy.py:136-150: optional neel X
     gates, then t periods of fast.py's U_F, no ancilla) under the depolarizing
-    channel after every kick gate and prep X, for t = 0..T-1."""
+    channel after every kick gate and prep X, for t = 0..T-1.  ``dev`` (a
+    DeviceNoise): the device-like channel instead (p unused), no read-out."""
     N = 1 << L
     x = np.arange(N)
     w = np.ones(N)
+    if dev is not None:
+        p = dev.site_channels()
     for i in range(L):
         flipped = initial_state == "neel" and (i + 1) % 2 == 0
-        pf = (1 - p / 2) if flipped else 0.0
+        pi = p[i][2] if dev is not None else p
+        pf = (1 - pi / 2) if flipped else 0.0
         b = (x >> i) & 1
         w = w * np.where(b == 1, pf, 1 - pf)
     rho = DM(L, np.diag(w).astype(np.complex128))

@@ -361,14 +361,22 @@ static uint32_t orc_u32(double prob) {
  * gamma = 1 - exp(-tg/T1); pure dephasing Z w.p. (1 - exp(-tg (1/T2 - 1/2T1)))/2
  * (T2 <= 2 T1); composite with depolarizing(p): X, Y p/4, Z (1-d) p/4 + d (1-3p/4);
  * jump w.p. q1 = gamma/2 with K1/sqrt(q1), else K0/sqrt(1 - q1). */
-int orc_autocorr_device(const orc_problem* pr, const orc_device_noise* dv, uint64_t seed,
-                        int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
-                        double* zsite, int32_t n_threads) {
-  const int L = pr->L;
-  uint32_t* thr = (uint32_t*)malloc(sizeof(uint32_t) * 3 * L);
-  uint32_t* jmp = (uint32_t*)malloc(sizeof(uint32_t) * L);
-  double* kr = (double*)malloc(sizeof(double) * 3 * L);
-  if (!thr || !jmp || !kr) { free(thr); free(jmp); free(kr); return -3; }
+typedef struct {
+  orc_rng rng;
+  uint32_t* thr;
+  uint32_t* jmp;
+  double* kr;
+} orc_device_rng;
+
+static void device_rng_free(orc_device_rng* d) {
+  free(d->thr); free(d->jmp); free(d->kr);
+}
+
+static int device_rng_init(orc_device_rng* d, const orc_device_noise* dv, int L, uint64_t seed) {
+  d->thr = (uint32_t*)malloc(sizeof(uint32_t) * 3 * L);
+  d->jmp = (uint32_t*)malloc(sizeof(uint32_t) * L);
+  d->kr = (double*)malloc(sizeof(double) * 3 * L);
+  if (!d->thr || !d->jmp || !d->kr) { device_rng_free(d); return -3; }
   for (int i = 0; i < L; ++i) {
     const double p = dv->p_gate[i];
     const double t1 = dv->t1_us[i] > 0.0 ? dv->t1_us[i] * 1e3 : INFINITY;
@@ -378,29 +386,72 @@ int orc_autocorr_device(const orc_problem* pr, const orc_device_noise* dv, uint6
     const double gamma = isinf(t1) ? 0.0 : 1.0 - exp(-tg / t1);
     double rate = (isinf(t2) ? 0.0 : 1.0 / t2) - (isinf(t1) ? 0.0 : 0.5 / t1);
     if (rate < 0.0) rate = 0.0;
-    const double d = 0.5 * (1.0 - exp(-tg * rate));
+    const double dd = 0.5 * (1.0 - exp(-tg * rate));
     const double px = p / 4.0, py = p / 4.0;
-    const double pz = (1.0 - d) * p / 4.0 + d * (1.0 - 3.0 * p / 4.0);
-    thr[3 * i + 0] = orc_u32(px);
-    thr[3 * i + 1] = orc_u32(px + py);
-    thr[3 * i + 2] = orc_u32(px + py + pz);
+    const double pz = (1.0 - dd) * p / 4.0 + dd * (1.0 - 3.0 * p / 4.0);
+    d->thr[3 * i + 0] = orc_u32(px);
+    d->thr[3 * i + 1] = orc_u32(px + py);
+    d->thr[3 * i + 2] = orc_u32(px + py + pz);
     const double q1 = gamma / 2.0, q0 = 1.0 - q1;
-    jmp[i] = orc_u32(q1);
-    kr[3 * i + 0] = 1.0 / sqrt(q0);
-    kr[3 * i + 1] = sqrt(1.0 - gamma) / sqrt(q0);
-    kr[3 * i + 2] = q1 > 0.0 ? sqrt(gamma / q1) : 0.0;
+    d->jmp[i] = orc_u32(q1);
+    d->kr[3 * i + 0] = 1.0 / sqrt(q0);
+    d->kr[3 * i + 1] = sqrt(1.0 - gamma) / sqrt(q0);
+    d->kr[3 * i + 2] = q1 > 0.0 ? sqrt(gamma / q1) : 0.0;
   }
-  orc_rng rng;
-  orc_rng_init(&rng, 0.0, seed);
-  rng.noisy = 1;
-  rng.dev_thr = thr;
-  rng.dev_jump = jmp;
-  rng.dev_kraus = kr;
-  const int rc = autocorr_run(pr, &rng, dv->anc_factor, 1.0 - dv->readout_p01 - dv->readout_p10,
+  orc_rng_init(&d->rng, 0.0, seed);
+  d->rng.noisy = 1;
+  d->rng.dev_thr = d->thr;
+  d->rng.dev_jump = d->jmp;
+  d->rng.dev_kraus = d->kr;
+  return 0;
+}
+
+int orc_autocorr_device(const orc_problem* pr, const orc_device_noise* dv, uint64_t seed,
+                        int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
+                        double* zsite, int32_t n_threads) {
+  orc_device_rng d;
+  if (device_rng_init(&d, dv, pr->L, seed)) return -3;
+  const int rc = autocorr_run(pr, &d.rng, dv->anc_factor, 1.0 - dv->readout_p01 - dv->readout_p10,
                               dv->readout_p10 - dv->readout_p01, traj_offset, n_traj, fwd, echo,
                               zsite, n_threads);
-  free(thr); free(jmp); free(kr);
+  device_rng_free(&d);
   return rc;
+}
+
+/* orc_apply_periods under device-like noise (the energy path's trajectories:
+ * the state's norm carries the Kraus importance weight). */
+int orc_apply_periods_device(const orc_problem* pr, const orc_device_noise* dv, uint64_t seed,
+                             int32_t inst, int64_t traj, uint32_t stream, int32_t first_period,
+                             int32_t n_periods, int32_t inverse, double* state,
+                             double* zsite_out) {
+  orc_device_rng d;
+  if (device_rng_init(&d, dv, pr->L, seed)) return -3;
+  cpx* psi = (cpx*)state;
+  for (int k = 1; k <= n_periods; ++k) {
+    if (inverse)
+      period_inverse(pr, &d.rng, inst, psi, first_period - k + 1, k, (uint64_t)traj, stream);
+    else
+      period_forward(pr, &d.rng, inst, psi, first_period + k - 1, (uint64_t)traj, stream);
+  }
+  if (zsite_out) measure_z(psi, pr->L, zsite_out);
+  device_rng_free(&d);
+  return 0;
+}
+
+/* Basis state after the noisy neel preparation of trajectory traj (dv NULL:
+ * depolarizing p). */
+int64_t orc_init_mask(const orc_problem* pr, double p, const orc_device_noise* dv,
+                      uint64_t seed, int64_t traj) {
+  if (dv) {
+    orc_device_rng d;
+    if (device_rng_init(&d, dv, pr->L, seed)) return -3;
+    const uint64_t m = init_mask(pr, &d.rng, (uint64_t)traj);
+    device_rng_free(&d);
+    return (int64_t)m;
+  }
+  orc_rng rng;
+  orc_rng_init(&rng, p, seed);
+  return (int64_t)init_mask(pr, &rng, (uint64_t)traj);
 }
 
 /* Exposed for the RNG contract test. */

@@ -6,6 +6,9 @@ Follows one noisy trajectory of the L-qubit energy circuit
 gate-by-gate periods (oracle/dtc_oracle.c via c_oracle.apply_periods, same
 Philox draws as the engine: forward stream 0, period counter = period) and
 evaluates <Z_i>, <Z_i Z_i+1>, <X_i> of the state after every period in numpy.
+Under device-like noise (spec.device) the periods are the C oracle's
+Kraus-weighted ones and the observables are the unnormalised (weighted)
+expectations, before any read-out error.
 """
 from __future__ import annotations
 
@@ -17,7 +20,10 @@ STREAM_PREP = 0xFFFFFFFF
 
 
 def prep_mask(spec, seed, traj):
-    """Noisy neel preparation (X then a Pauli draw: X/Y undo the flip)."""
+    """Noisy neel preparation (X then a Pauli draw: X/Y undo the flip; under
+    device-like noise the draw of the C oracle's composite channel)."""
+    if getattr(spec, "device", None) is not None:
+        return c_oracle.init_mask(spec, seed, traj)
     m = spec.init_mask
     if spec.p > 0:
         for i in range(spec.L):

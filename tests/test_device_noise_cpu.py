@@ -99,3 +99,67 @@ def test_standin_calibration(pkg):
     assert all(0 < g < 1e-3 and 0 <= d < 1e-3 for g, d, _ in ch)
     with pytest.raises(ValueError):
         cal.device_noise(21)
+
+
+# ---- energy path under device-like noise (energy-fakebrisbane.py) ---------------
+
+def test_readout_observables_exact(pkg):
+    """The affine read-out map on Z, ZZ equals flipping every measured bit of an
+    arbitrary distribution independently (p01: 0 -> 1, p10: 1 -> 0)."""
+    rng = np.random.default_rng(4)
+    L = 3
+    prob = rng.random(1 << L)
+    prob /= prob.sum()
+    p01, p10 = np.array([0.02, 0.05, 0.01]), np.array([0.03, 0.01, 0.07])
+    flip = np.zeros((1 << L, 1 << L))   # flip[y, x] = P(read y | state x)
+    for xs in range(1 << L):
+        for ys in range(1 << L):
+            pr = 1.0
+            for i in range(L):
+                bx, by = (xs >> i) & 1, (ys >> i) & 1
+                pr *= (p01[i] if by else 1 - p01[i]) if bx == 0 else (1 - p10[i] if by else p10[i])
+            flip[ys, xs] = pr
+    read = flip @ prob
+    zs = lambda d, i: sum(d[x] * (1 - 2 * ((x >> i) & 1)) for x in range(1 << L))
+    zzs = lambda d, i: sum(d[x] * (1 - 2 * ((x >> i) & 1)) * (1 - 2 * ((x >> (i + 1)) & 1))
+                           for x in range(1 << L))
+    obs = {"z": np.array([zs(prob, i) for i in range(L)]),
+           "zz": np.array([zzs(prob, i) for i in range(L - 1)]), "x": np.zeros(L)}
+    got = pkg.energy.readout_observables(obs, p01, p10)
+    np.testing.assert_allclose(got["z"], [zs(read, i) for i in range(L)], atol=1e-15)
+    np.testing.assert_allclose(got["zz"], [zzs(read, i) for i in range(L - 1)], atol=1e-15)
+    np.testing.assert_allclose(got["x"], p10 - p01, atol=1e-15)
+
+
+def test_oracle_init_mask_matches_restatement(pkg):
+    from oracle import energy_oracle
+
+    rng = np.random.default_rng(2)
+    hs, phis = random_disorder(rng, 7)
+    spec = pkg.SweepSpec(L=7, T=2, hs=hs, phis=phis, g=0.9, noise_prob=0.4, initial_state="neel")
+    import dataclasses
+
+    plain = dataclasses.replace(spec)
+    plain.device = None
+    for tr in range(40):
+        assert c_oracle.init_mask(plain, 17, tr) == energy_oracle.prep_mask(plain, 17, tr)
+
+
+@pytest.mark.parametrize("state", ["vacuum", "neel"])
+def test_energy_oracle_device_trajectories_match_exact(pkg, state):
+    """Kraus-weighted energy trajectories of the oracle average to the exact
+    density matrix of the device-like channel (Z, ZZ, X every period)."""
+    from oracle import energy_oracle
+
+    rng = np.random.default_rng(21)
+    L, T, n = 4, 5, 3000
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, initial_state=state)
+    spec.device = harsh_device(pkg, L)
+    exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, 0.0, initial_state=state,
+                                   dev=spec.device)
+    runs = [energy_oracle.trajectory_energy(spec, 0, tr, seed=8) for tr in range(n)]
+    for k in range(3):
+        v = np.array([r[k] for r in runs])
+        mean, sd = v.mean(axis=0), v.std(axis=0) / np.sqrt(n) + 1e-12
+        assert np.all(np.abs(mean - exact[k]) < 5 * sd), k

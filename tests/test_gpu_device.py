@@ -156,3 +156,73 @@ def test_device_infinite_t1_is_pauli_noise(pkg, engine):
         a = out[key][0]
         z = (a.mean(axis=0) - exact) / (a.std(axis=0, ddof=1) / np.sqrt(4096) + 1e-12)
         assert np.max(np.abs(z)) < 4.5, (key, z)
+
+
+# ---- energy path under device-like noise (dtc_energy_device) --------------------
+
+@pytest.mark.parametrize("L,T,n_traj,state,pol", [
+    (4, 6, 4, "neel", "x"),
+    (7, 5, 3, "vacuum", "xy"),
+    (13, 4, 2, "neel", "y"),
+    (20, 3, 2, "vacuum", "x"),
+])
+def test_device_energy_matches_oracle(pkg, engine, L, T, n_traj, state, pol):
+    from oracle import energy_oracle
+
+    rng = np.random.default_rng(L + 40)
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.92, polarization=pol,
+                         initial_state=state, device=harsh_device(pkg, L))
+    got = engine.energy(spec, n_traj, seed=13)
+    for tr in range(n_traj):
+        z, zz, x = energy_oracle.trajectory_energy(spec, 0, tr, seed=13)
+        assert np.abs(got["z"][0, tr] - z).max() < 1e-10
+        assert np.abs(got["zz"][0, tr] - zz).max() < 1e-10
+        assert np.abs(got["x"][0, tr] - x).max() < 1e-10
+
+
+def test_device_energy_means_match_exact_dm(pkg, engine):
+    rng = np.random.default_rng(5)
+    L, T, n = 4, 6, 8192
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.95, initial_state="neel",
+                         device=harsh_device(pkg, L))
+    exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, 0.0, initial_state="neel",
+                                   dev=spec.device)
+    got = engine.energy(spec, n, seed=77, batch=1000)
+    for k, key in enumerate(("z", "zz", "x")):
+        v = got[key][0]
+        se = v.std(axis=0, ddof=1) / np.sqrt(n) + 1e-12
+        z = (v.mean(axis=0) - exact[k]) / se
+        assert np.max(np.abs(z)) < 4.5, (key, z)
+
+
+def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
+    """energy_cli --use_fakebackend 1 (energy-fakebrisbane.py): folder
+    energy-data_L4-fakebrisbane, column energy_p_fakebrisbane = <H>(t) with
+    per-site read-out error, not divided by L."""
+    import pandas as pd
+
+    d = golden["disorder"]["L4"]
+    dis = tmp_path / "dis"
+    dis.mkdir()
+    pd.DataFrame(d["hs"]).to_csv(dis / "hs_L4.csv", index=False)
+    pd.DataFrame(d["phis"]).to_csv(dis / "phis_L4.csv", index=False)
+    out = tmp_path / "out"
+    rc = pkg.energy_cli.main(["--L", "4", "--tf", "4", "--use_fakebackend", "1",
+                              "--trajectories", "32", "--disorder_folder", str(dis),
+                              "--out_dir", str(out)])
+    assert rc == 0
+    files = list((out / "energy-data_L4-fakebrisbane").glob("energy_data_*.csv"))
+    assert len(files) == 1
+    df = pd.read_csv(files[0])
+    assert list(df.columns) == ["time", "energy_p_fakebrisbane"]
+    # t = 0: the vacuum |0000> read out with the per-site flips
+    cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data", "device_standin_L20.json"))
+    p01, p10 = cal.site_readout(4)
+    obs = {"z": np.ones(4), "zz": np.ones(3), "x": np.zeros(4)}
+    ro = pkg.energy.readout_observables(obs, p01, p10)
+    hs = np.array(d["hs"])[0, :4]
+    phis = np.array(d["phis"])[0, :3]
+    e0 = pkg.energy.energy_from_observables(ro, 4, 0.97, hs, phis, "full")
+    assert df["energy_p_fakebrisbane"][0] == pytest.approx(float(e0), abs=1e-12)
