@@ -109,6 +109,7 @@ class PointEstimator:
     shots: int = 1024
     seed: int = 0x5EED0001
     engine: object = None
+    device: object = None  # DeviceNoise (use_fakebackend=1), or None
     calls: int = field(default=0)
 
     def _eng(self):
@@ -124,11 +125,12 @@ class PointEstimator:
         t = len(g_list) - 1
         spec = SweepSpec(L=self.L, T=t + 1, hs=self.hs[None, :], phis=self.phis[None, :],
                          g=[float(x) for x in g_list], noise_prob=self.noise_prob,
-                         use_noise=self.use_noise, initial_state=self.initial_state, t_offset=1)
+                         use_noise=self.use_noise, initial_state=self.initial_state, t_offset=1,
+                         device=self.device)
         ss = np.random.SeedSequence([self.seed & 0xFFFFFFFF, self.seed >> 32, self.calls])
         self.calls += 1
         s64 = int(ss.generate_state(1, dtype=np.uint64)[0])
-        noisy = spec.p > 0
+        noisy = spec.p > 0 or self.device is not None
         n_traj = self.shots if noisy else 1
         out = self._eng().autocorr(spec, n_traj, seed=s64, want_fwd=want_fwd,
                                    want_echo=want_echo, t_first=t)
@@ -139,8 +141,15 @@ class PointEstimator:
                 res.append(None)
                 continue
             a = out[key][:, :, t:t + 1]
-            res.append(float(_shot_estimate(a, self.shots, rng)[0, 0]) if self.shots
-                       else float(a.mean()))
+            if not self.shots:
+                res.append(float(a.mean()))
+            elif self.device is not None:
+                # importance-weighted trajectories are not per-shot probabilities:
+                # the shots are drawn from the trajectory mean (as sweep.run_sweep)
+                m = min(1.0, max(0.0, (1.0 + float(a.mean())) / 2.0))
+                res.append((2.0 * rng.binomial(self.shots, m) - self.shots) / self.shots)
+            else:
+                res.append(float(_shot_estimate(a, self.shots, rng)[0, 0]))
         return tuple(res)
 
 
@@ -174,8 +183,9 @@ class AdaptiveResult:
 
 def realtime_adaptive(L, T, hs, phis, g_initial, cfg: ControllerConfig, noise_prob=0.05,
                       use_noise=1, initial_state="vacuum", shots=1024, seed=0x5EED0001,
-                      engine=None, log=None) -> AdaptiveResult:
-    """get_instances_adaptive_realtime (ctrlg.py:423-532, gopt.py:497-623)."""
+                      engine=None, log=None, device=None) -> AdaptiveResult:
+    """get_instances_adaptive_realtime (ctrlg.py:423-532, gopt.py:497-623).
+    ``device``: DeviceNoise for ``--use_fakebackend 1`` (ctrlg.py:246-250)."""
     hs = np.atleast_2d(hs)
     phis = np.atleast_2d(phis)
     n_inst = hs.shape[0]
@@ -184,7 +194,7 @@ def realtime_adaptive(L, T, hs, phis, g_initial, cfg: ControllerConfig, noise_pr
     gs = np.zeros((n_inst, T))
     for i in range(n_inst):
         est = PointEstimator(L, hs[i, :L], phis[i, :L - 1], noise_prob, use_noise, initial_state,
-                             shots, seed + 7919 * i, engine)
+                             shots, seed + 7919 * i, engine, device)
         hist = []
         g = float(g_initial)
         for t in range(T):
@@ -200,15 +210,16 @@ def realtime_adaptive(L, T, hs, phis, g_initial, cfg: ControllerConfig, noise_pr
 
 
 def fixed_g_sweep(L, T, hs, phis, g, noise_prob=0.05, use_noise=1, initial_state="vacuum",
-                  shots=1024, seed=0x5EED0001, engine=None):
+                  shots=1024, seed=0x5EED0001, engine=None, device=None):
     """get_instances with a fixed g (ctrlg.py:583-601): all t in one engine
     sweep, t+1 periods at time t.  Returns (forward, echo), each [inst][T]."""
     from . import sweep as sw
 
     spec = SweepSpec(L=L, T=T, hs=np.atleast_2d(hs), phis=np.atleast_2d(phis), g=float(g),
                      noise_prob=noise_prob, use_noise=use_noise, initial_state=initial_state,
-                     t_offset=1)
-    r = sw.run_sweep(spec, shots=shots if spec.p > 0 else None, engine=engine, seed=seed)
+                     t_offset=1, device=device)
+    noisy = spec.p > 0 or device is not None
+    r = sw.run_sweep(spec, shots=shots if noisy else None, engine=engine, seed=seed)
     return r.fwd, r.echo
 
 

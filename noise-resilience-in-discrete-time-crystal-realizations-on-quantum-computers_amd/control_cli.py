@@ -33,7 +33,11 @@ def build_parser(script="controlled-g"):
     p.add_argument("--noise_prob", type=float, default=0.05)
     p.add_argument("--use_noise", type=int, default=1)
     p.add_argument("--initial_state", type=str, default="vacuum", choices=["vacuum", "neel"])
-    p.add_argument("--use_fakebackend", type=int, default=0)
+    p.add_argument("--use_fakebackend", type=int, default=0,
+                   help="1: device-like noise from --device_calibration (FakeBrisbane's own "
+                        "calibration is not available offline)")
+    p.add_argument("--device_calibration", type=str, default=None,
+                   help="calibration JSON for --use_fakebackend 1 (default: the stand-in)")
     p.add_argument("--target_echo", type=float, default=1.0)
     p.add_argument("--feedback_gain", type=float, default=0.01)
     p.add_argument("--exponential_feedback", type=int, default=1)
@@ -54,8 +58,6 @@ def main(argv=None):
     pre.add_argument("--script", choices=tuple(DEFAULTS), default="controlled-g")
     known, _ = pre.parse_known_args(argv)
     args = build_parser(known.script).parse_args(argv)
-    if args.use_fakebackend:
-        raise SystemExit("use_fakebackend=1: FakeBrisbane calibration data is not available offline")
     if args.script == "controlled-g" and args.use_optimization:
         raise SystemExit("--use_optimization belongs to --script g-optimization")
     cfg = ct.ControllerConfig(args.target_echo, args.feedback_gain, args.exponential_feedback,
@@ -63,8 +65,19 @@ def main(argv=None):
                               args.use_optimization, args.optimization_iterations)
     L, T = args.L, args.tf
     hs, phis = load_disorder(L, args.inst, args.disorder_folder)
+    device = None
+    if args.use_fakebackend:
+        # ctrlg.py:246-250 runs on FakeBrisbane(); its calibration is not
+        # available offline: device-like noise from a calibration file
+        from .cli import DEFAULT_CALIBRATION
+        from .device_noise import DeviceCalibration
+
+        cal_path = args.device_calibration or DEFAULT_CALIBRATION
+        cal = DeviceCalibration.from_json(cal_path)
+        print(f"Device-like noise from {cal_path} ({cal.name})")
+        device = cal.device_noise(L)
     common = dict(noise_prob=args.noise_prob, use_noise=args.use_noise,
-                  initial_state=args.initial_state, shots=args.shots)
+                  initial_state=args.initial_state, shots=args.shots, device=device)
     ad = ct.realtime_adaptive(L, T, hs, phis, args.g, cfg, seed=args.seed, log=print, **common)
     std84 = ct.fixed_g_sweep(L, T, hs, phis, args.g, seed=args.seed + 1, **common)
     std97 = ct.fixed_g_sweep(L, T, hs, phis, 0.97, seed=args.seed + 2, **common)

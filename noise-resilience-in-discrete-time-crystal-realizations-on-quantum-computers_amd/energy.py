@@ -169,15 +169,29 @@ def energy_csv_name(prefix, state, g, L, inst, randomphi, delta, amplitude, nois
 
 def run_energy(L, g, hs, phis, T, nprobs=(0, 0.001, 0.01, 0.1), use_noise=1,
                initial_state="vacuum", n_traj=ESTIMATOR_SHOTS, seed=0x5EED0001,
-               hamiltonian_types=("full",), accumulate=True, engine=None):
+               hamiltonian_types=("full",), accumulate=True, engine=None, calibration=None):
     """energy.py's main loop (:212-222): for each nprob, ``av_energy / L`` per
-    Hamiltonian variant.  Returns ``{(ht, nprob): [T]}``."""
+    Hamiltonian variant.  Returns ``{(ht, nprob): [T]}``.
+
+    ``calibration`` (a DeviceCalibration): ``--use_fakebackend 1`` of these
+    scripts — ``NoiseModel.from_backend(FakeBrisbane())`` on the simulator,
+    where the loop adds no depolarizing error (energy.py:74-78, 214-218): every
+    nprob column is the device-noise run (its own shots; here its own seed),
+    with per-site read-out error."""
     eff = accumulated_noise(nprobs) if accumulate else [float(p) for p in nprobs]
     res = {}
-    for nprob, p_eff in zip(nprobs, eff):
+    for k, (nprob, p_eff) in enumerate(zip(nprobs, eff)):
         spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
-                         noise_prob=p_eff, use_noise=use_noise)
-        per = get_instances_energy(spec, n_traj, hamiltonian_types, seed, engine)
+                         noise_prob=0.0 if calibration is not None else p_eff,
+                         use_noise=1 if calibration is not None else use_noise)
+        readout = None
+        run_seed = seed
+        if calibration is not None:
+            spec.device = calibration.device_noise(L)
+            readout = calibration.site_readout(L)
+            run_seed = seed + 7919 * k
+        per = get_instances_energy(spec, n_traj, hamiltonian_types, run_seed, engine,
+                                   readout=readout)
         for ht, v in per.items():
             res[(ht, nprob)] = v.mean(axis=0) / L
     return res
@@ -189,12 +203,16 @@ def run_energy_device(L, g, hs, phis, T, calibration, initial_state="vacuum",
     device's noise (here: device-like noise from a calibration file, see
     device_noise.py; FakeBrisbane's own data is unavailable offline), read-out
     error on every measured site, mean over instances — NOT divided by L (the
-    script saves ``np.mean(energy, axis=0)`` as is)."""
+    script saves ``np.mean(energy, axis=0)`` as is).  ``calibration=None``:
+    the script with ``--use_fakebackend 0`` (an empty NoiseModel: noiseless)."""
     spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
-                     noise_prob=0.0, use_noise=1)
-    spec.device = calibration.device_noise(L)
-    per = get_instances_energy(spec, n_traj, ("full",), seed, engine,
-                               readout=calibration.site_readout(L))["full"]
+                     noise_prob=0.0, use_noise=1 if calibration is not None else 0)
+    readout = None
+    if calibration is not None:
+        spec.device = calibration.device_noise(L)
+        readout = calibration.site_readout(L)
+    per = get_instances_energy(spec, n_traj if calibration is not None else 1, ("full",), seed,
+                               engine, readout=readout)["full"]
     return per.mean(axis=0)
 
 

@@ -80,7 +80,7 @@ def run_sweep(spec: SweepSpec, n_traj: int | None = None, shots: int | None = No
     """All t of all instances in one engine call."""
     eng = engine or _default_engine()
     if n_traj is None:
-        n_traj = 1 if spec.p == 0 else (shots or 1024)
+        n_traj = 1 if (spec.p == 0 and spec.device is None) else (shots or 1024)
     out = eng.autocorr(spec, n_traj, seed=seed, traj_offset=traj_offset, want_fwd=want_fwd,
                        want_echo=want_echo, want_zsite=want_zsite, batch=batch)
     rng = np.random.default_rng(seed)

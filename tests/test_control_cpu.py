@@ -109,3 +109,26 @@ def test_realtime_loop_and_outputs(pkg, golden, tmp_path, opt):
         assert "adaptive_optimization_vs_fixed" in os.path.basename(comp)
     else:
         assert "_exp0.1_" in os.path.basename(main)
+
+
+def test_realtime_loop_device_noise(pkg, golden):
+    """Device-like noise through the controllers (the C oracle as the engine):
+    estimates come from shots drawn on the trajectory mean, and the loop's
+    first estimate matches the exact density matrix within shot noise."""
+    from oracle import dm_oracle
+
+    ct = pkg.control
+    d = golden["disorder"]["L4"]
+    hs, phis = np.array(d["hs"])[:, :4], np.array(d["phis"])[:, :3]
+    dev = pkg.DeviceNoise(p_gate=np.full(4, 0.02), t1_us=np.full(4, 2.0), t2_us=np.full(4, 2.5),
+                          gate_ns=120.0, anc_factor=0.9, readout_p01=0.02, readout_p10=0.03)
+    cfg = ct.ControllerConfig(feedback_gain=0.05, exponential_feedback=1, g_max=0.95)
+    eng = OracleEngine()
+    ad = ct.realtime_adaptive(4, 3, hs, phis, 0.84, cfg, shots=2048, engine=eng, device=dev)
+    assert ad.g[0, 0] == 0.84 and np.all((ad.g >= 0.84) & (ad.g <= 0.95))
+    spec = pkg.SweepSpec(L=4, T=1, hs=hs[:1], phis=phis[:1], g=[0.84], t_offset=1)
+    fe, ee = dm_oracle.device_folded_sweep(4, 1, hs[0], phis[0], spec.kick, dev, t_offset=1)
+    sd = 1.0 / np.sqrt(2048)
+    assert abs(ad.forward[0, 0] - fe[0]) < 5 * sd and abs(ad.echo[0, 0] - ee[0]) < 5 * sd
+    f84, e84 = ct.fixed_g_sweep(4, 3, hs, phis, 0.84, shots=256, engine=eng, device=dev)
+    assert f84.shape == (1, 3) and np.all(np.abs(e84) <= 1)

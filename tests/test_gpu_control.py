@@ -61,3 +61,26 @@ def test_control_cli(pkg, golden, tmp_path, script, extra):
     assert len(files) == 2
     main = pd.read_csv(out / "controlled-autocorr_data_L4" / files[0])
     assert len(main) == 6 and main["g_history_inst1"][0] == 0.84
+
+
+def test_control_cli_use_fakebackend(pkg, golden, tmp_path):
+    """--use_fakebackend 1 (ctrlg.py:246-250 on FakeBrisbane): device-like noise
+    from the stand-in calibration drives the realtime loop and the fixed-g
+    comparisons; same folder and files."""
+    import pandas as pd
+
+    d = golden["disorder"]["L4"]
+    dis = tmp_path / "dis"
+    dis.mkdir()
+    pd.DataFrame(d["hs"]).to_csv(dis / "hs_L4.csv", index=False)
+    pd.DataFrame(d["phis"]).to_csv(dis / "phis_L4.csv", index=False)
+    out = tmp_path / "out"
+    rc = pkg.control_cli.main(["--L", "4", "--inst", "1", "--tf", "5", "--shots", "256",
+                               "--use_fakebackend", "1", "--disorder_folder", str(dis),
+                               "--out_dir", str(out)])
+    assert rc == 0
+    files = sorted(os.listdir(out / "controlled-autocorr_data_L4"))
+    assert len(files) == 2
+    main = pd.read_csv(out / "controlled-autocorr_data_L4" / files[0])
+    assert len(main) == 5 and main["g_history_inst1"][0] == 0.84
+    assert np.all(np.abs(main["av_autocorr_echo_adaptive"]) <= 1.0)

@@ -198,9 +198,11 @@ def test_device_energy_means_match_exact_dm(pkg, engine):
 
 
 def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
-    """energy_cli --use_fakebackend 1 (energy-fakebrisbane.py): folder
-    energy-data_L4-fakebrisbane, column energy_p_fakebrisbane = <H>(t) with
-    per-site read-out error, not divided by L."""
+    """energy_cli --mode fakebrisbane (energy-fakebrisbane.py, whose
+    --use_fakebackend defaults to 1): folder energy-data_L4-fakebrisbane,
+    column energy_p_fakebrisbane = <H>(t) with per-site read-out error, not
+    divided by L.  Then energy.py with --use_fakebackend 1: every nprob column
+    is the device-noise run, divided by L."""
     import pandas as pd
 
     d = golden["disorder"]["L4"]
@@ -209,7 +211,7 @@ def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
     pd.DataFrame(d["hs"]).to_csv(dis / "hs_L4.csv", index=False)
     pd.DataFrame(d["phis"]).to_csv(dis / "phis_L4.csv", index=False)
     out = tmp_path / "out"
-    rc = pkg.energy_cli.main(["--L", "4", "--tf", "4", "--use_fakebackend", "1",
+    rc = pkg.energy_cli.main(["--mode", "fakebrisbane", "--L", "4", "--tf", "4",
                               "--trajectories", "32", "--disorder_folder", str(dis),
                               "--out_dir", str(out)])
     assert rc == 0
@@ -226,3 +228,11 @@ def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
     phis = np.array(d["phis"])[0, :3]
     e0 = pkg.energy.energy_from_observables(ro, 4, 0.97, hs, phis, "full")
     assert df["energy_p_fakebrisbane"][0] == pytest.approx(float(e0), abs=1e-12)
+    rc = pkg.energy_cli.main(["--mode", "full", "--use_fakebackend", "1", "--L", "4", "--tf", "4",
+                              "--trajectories", "32", "--disorder_folder", str(dis),
+                              "--out_dir", str(out)])
+    assert rc == 0
+    full = list((out / "energy-data_L4-full-ham").glob("energy_data_*.csv"))
+    df = pd.read_csv(full[0])
+    for p in ("0", "0.001", "0.01", "0.1"):
+        assert df[f"energy_p_{p}"][0] == pytest.approx(float(e0) / 4, abs=1e-12)

@@ -98,9 +98,20 @@ def test_energy_cli_files(pkg, golden, tmp_path, mode, cols):
                               "--disorder_folder", str(dis), "--out_dir", str(out)])
     assert rc == 0
     files = [os.path.join(r, f) for r, _, fs in os.walk(out) for f in fs]
-    assert len(files) == 1
-    df = pd.read_csv(files[0])
+    main = [f for f in files if not os.path.basename(f).startswith("comprehensive")]
+    assert len(main) == 1
+    df = pd.read_csv(main[0])
     assert list(df.columns) == cols and len(df) == 6
+    if mode == "vs-echo":
+        # vs-echo.py:436-448 without an autocorr CSV next to it (and its default
+        # --use_fakebackend 1: device-like noise from the stand-in calibration)
+        comp = [f for f in files if os.path.basename(f).startswith("comprehensive_data_energy_only")]
+        assert len(comp) == 1
+        c = pd.read_csv(comp[0])
+        assert list(c.columns) == ["time", "energy_with_x", "energy_without_x"]
+        assert np.allclose(c["energy_with_x"], df["energy_with_x_p_0.1"])
+    else:
+        assert len(files) == 1
     if mode == "full":
         # t = 0: <H>/L of the vacuum = (sum h_i + sum phi_i) / L  (X terms vanish)
         hs, phis = pkg.load_disorder(4, 1, str(dis))
