@@ -120,6 +120,11 @@ def main():
                          "energy: the energy observable path (§8(f)1); ctrl: the real-time "
                          "adaptive-g controller loop (§8(f)2)")
     ap.add_argument("--ctrl-tf", type=int, default=20, help="ctrl: time points of the loop")
+    ap.add_argument("--ctrl-opt", action="store_true",
+                    help="ctrl: the optimisation controller (g-optimization.py) instead of "
+                         "the feedback rule; value = controller time points per second")
+    ap.add_argument("--no-prefix-cache", action="store_true",
+                    help="ctrl --ctrl-opt: a full t+1-period run per candidate evaluation")
     ap.add_argument("--shard-bits", type=int, default=3, help="c5: log2 of the shard count")
     ap.add_argument("--instances", type=int, default=32, help="c4: instances per step per GPU")
     args = ap.parse_args()
@@ -649,7 +654,8 @@ def main_ctrl(args):
     pkg = importlib.import_module(PKG)
     L, T, shots = args.L, args.ctrl_tf, 1024
     eng = pkg.DtcEngine(local_rank)
-    cfg = pkg.control.ControllerConfig()
+    cfg = pkg.control.ControllerConfig(use_optimization=int(args.ctrl_opt),
+                                       prefix_cache=0 if args.no_prefix_cache else 1)
     hs, phis = load_disorder_row(L)
     res_g = np.zeros((1, T))
 
@@ -670,29 +676,43 @@ def main_ctrl(args):
     # the same kernel (probe measurement) as C2: its PMC ratio, scaled
     roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"])
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    # (the optimisation loop's evaluation count is data-dependent: no fixed CPU work unit)
+    if world == 1 and not args.no_cpu_baseline and not args.ctrl_opt:
         hs_, phis_ = load_disorder_row(L)
         s = pkg.SweepSpec(L=L, T=args.cpu_tf, hs=hs_, phis=phis_, g=0.84, noise_prob=0.05,
                           use_noise=1, t_offset=1)
         cpu = cpu_baseline(s, args.cpu_traj or 2 * _host_threads(), args.cpu_tf,
                            _host_threads(), t_offset=1)
         cpu["unit"] = "periods*trajectories/s"
-    res = {
-        "metric": "Floquet-periods×trajectories/sec of the L=20 real-time adaptive-g loop "
-                  "(controlled-g); RZZ-kernel HBM GB/s vs peak",
-        "value": n_loops * per_loop / elapsed, "unit": "periods*trajectories/s",
+    if args.ctrl_opt:
+        pc = "without" if args.no_prefix_cache else "with"
+        head = {
+            "metric": (f"controller time points/sec of the L={L} optimisation loop "
+                       "(g-optimization); RZZ-kernel HBM GB/s vs peak"),
+            "value": n_loops * T / elapsed, "unit": "time points/s"}
+        workload = (f"optimisation controller (§8(f)2, bounded Brent per t, {pc} the forward "
+                    f"prefix cache): L={L}, g_initial=0.84, p=0.05, tf={T}, {shots} "
+                    f"trajectories per evaluation, one closed loop per step per GPU")
+    else:
+        head = {
+            "metric": "Floquet-periods×trajectories/sec of the L=20 real-time adaptive-g loop "
+                      "(controlled-g); RZZ-kernel HBM GB/s vs peak",
+            "value": n_loops * per_loop / elapsed, "unit": "periods*trajectories/s"}
+        workload = (f"adaptive-g controller (§8(f)2): L={L}, g_initial=0.84, p=0.05, "
+                    f"tf={T}, {shots} trajectories per estimate, exponential "
+                    f"feedback (gain 0.01), one closed loop per step per GPU")
+    res = dict(head)
+    res.update({
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (disorder row 0 of hs/phis_L20.csv)",
-        "config": {"workload": (f"adaptive-g controller (§8(f)2): L={L}, g_initial=0.84, p=0.05, "
-                                f"tf={T}, {shots} trajectories per estimate, exponential "
-                                f"feedback (gain 0.01), one closed loop per step per GPU"),
+        "config": {"workload": workload,
                    "L": L, "tf": T, "shots": shots, "parallelism": f"instance-sharded x{world}"},
         "roofline": roof, "kernels": kern,
         "ms_per_time_point": elapsed / (args.steps * T) * 1e3,
         "g_history_mean": (acc[0] / n_loops).tolist(),
         "device": eng.device_info()["name"],
-    }
+    })
     if cpu:
         res["cpu_baseline"] = cpu
     print(json.dumps(res), flush=True)

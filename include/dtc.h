@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 4
+#define DTC_ABI_VERSION 5
 
 /* error codes */
 #define DTC_OK 0
@@ -195,6 +195,28 @@ int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise
 /* Host-only: the site groups the engine's passes use for an n_bits-bit state
  * (bit masks, one per group; returns the count or a negative error). */
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups);
+
+/* Forward prefix cache (the optimisation controller, SURVEY.md §8(f) row 2:
+ * -g-optimization.py:359-427 re-runs the t+1-period circuit for every
+ * candidate g of the last period; the t-period forward part is the same for
+ * all candidates).
+ * dtc_prefix_build: take the n_inst * n_traj trajectories (traj_offset ..)
+ * of prob through periods 1..n_periods (noise keyed by seed, neel prep
+ * included) and keep their states on the device, replacing any previous
+ * prefix.  noise or dv (device-like noise, then noise is ignored).
+ * dtc_autocorr_prefixed: dtc_autocorr (dv: dtc_autocorr_device, no zsite)
+ * starting from those states: periods > n_periods and every echo draw their
+ * noise from seed, the prefix periods keep theirs.  prob must match the
+ * prefix's (instances, angles, kick rows 1..n_periods: checked by hash; the
+ * same trajectories) and measure only after it (t_first + t_offset >
+ * n_periods).  dtc_prefix_release frees the states. */
+int dtc_prefix_build(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                     const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                     int32_t n_traj, int32_t n_periods);
+int dtc_autocorr_prefixed(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                          const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                          int32_t n_traj, double* fwd, double* echo);
+int dtc_prefix_release(dtc_ctx* ctx);
 
 /* Energy observables of the forward sweep (the
  * BackendEstimatorV2 runs of autocorr-delta-a-single-qiskit-fast-energy*.py:

@@ -33,6 +33,9 @@ EXPORTED_SYMBOLS = (
     "dtc_energy",
     "dtc_autocorr_device",
     "dtc_energy_device",
+    "dtc_prefix_build",
+    "dtc_autocorr_prefixed",
+    "dtc_prefix_release",
 )
 
 KERNEL_LO_PASS = 0
@@ -170,6 +173,15 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_void_p, P(DtcProblem), P(DtcDeviceNoise), ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_int32, _dp, _dp, _dp,
         ]
+        lib.dtc_prefix_build.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcDeviceNoise), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+        ]
+        lib.dtc_autocorr_prefixed.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcDeviceNoise), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, _dp, _dp,
+        ]
+        lib.dtc_prefix_release.argtypes = [ctypes.c_void_p]
         lib.dtc_plan_groups.argtypes = [ctypes.c_int32, P(ctypes.c_uint64), ctypes.c_int32]
         for name in EXPORTED_SYMBOLS:
             if name not in ("dtc_last_error", "dtc_abi_version"):

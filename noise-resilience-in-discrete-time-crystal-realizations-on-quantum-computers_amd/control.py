@@ -48,6 +48,10 @@ class ControllerConfig:
     g_max: float = 1.0
     use_optimization: int = 0
     optimization_iterations: int = 5  # accepted for fidelity; unused by the reference too
+    # optimisation: build the t-period forward states once per t and run only
+    # the candidate's last period + echo per evaluation (dtc_prefix_*); the
+    # candidates then share the prefix's noise draws (common random numbers)
+    prefix_cache: int = 1
 
     @property
     def method_suffix(self) -> str:
@@ -111,6 +115,7 @@ class PointEstimator:
     engine: object = None
     device: object = None  # DeviceNoise (use_fakebackend=1), or None
     calls: int = field(default=0)
+    prefix_periods: int = field(default=0)  # > 0: a prefix of that many periods is built
 
     def _eng(self):
         if self.engine is None:
@@ -119,21 +124,46 @@ class PointEstimator:
             self.engine = sweep._default_engine()
         return self.engine
 
+    def _spec(self, g_list):
+        return SweepSpec(L=self.L, T=len(g_list), hs=self.hs[None, :], phis=self.phis[None, :],
+                         g=[float(x) for x in g_list], noise_prob=self.noise_prob,
+                         use_noise=self.use_noise, initial_state=self.initial_state, t_offset=1,
+                         device=self.device)
+
+    def _n_traj(self, spec):
+        return self.shots if (spec.p > 0 or self.device is not None) else 1
+
+    def build_prefix(self, g_prefix):
+        """Forward states after the len(g_prefix) periods every candidate of
+        optimize_g shares (own seed, as one more independent run)."""
+        spec = self._spec(g_prefix)
+        ss = np.random.SeedSequence([self.seed & 0xFFFFFFFF, self.seed >> 32, self.calls])
+        self.calls += 1
+        s64 = int(ss.generate_state(1, dtype=np.uint64)[0])
+        self._eng().prefix_build(spec, self._n_traj(spec), len(g_prefix), seed=s64)
+        self.prefix_periods = len(g_prefix)
+
+    def release_prefix(self):
+        if self.prefix_periods:
+            self._eng().prefix_release()
+        self.prefix_periods = 0
+
     def __call__(self, g_list, want_fwd=True, want_echo=True):
         from .sweep import _shot_estimate
 
         t = len(g_list) - 1
-        spec = SweepSpec(L=self.L, T=t + 1, hs=self.hs[None, :], phis=self.phis[None, :],
-                         g=[float(x) for x in g_list], noise_prob=self.noise_prob,
-                         use_noise=self.use_noise, initial_state=self.initial_state, t_offset=1,
-                         device=self.device)
+        spec = self._spec(g_list)
         ss = np.random.SeedSequence([self.seed & 0xFFFFFFFF, self.seed >> 32, self.calls])
         self.calls += 1
         s64 = int(ss.generate_state(1, dtype=np.uint64)[0])
-        noisy = spec.p > 0 or self.device is not None
-        n_traj = self.shots if noisy else 1
-        out = self._eng().autocorr(spec, n_traj, seed=s64, want_fwd=want_fwd,
-                                   want_echo=want_echo, t_first=t)
+        n_traj = self._n_traj(spec)
+        if self.prefix_periods and self.prefix_periods == t:
+            # the prefix holds periods 1..t: only period t+1 and the echo run
+            out = self._eng().autocorr_prefixed(spec, n_traj, seed=s64, want_fwd=want_fwd,
+                                                want_echo=want_echo, t_first=t)
+        else:
+            out = self._eng().autocorr(spec, n_traj, seed=s64, want_fwd=want_fwd,
+                                       want_echo=want_echo, t_first=t)
         rng = np.random.default_rng(ss.spawn(1)[0])
         res = []
         for key, want in (("fwd", want_fwd), ("echo", want_echo)):
@@ -155,21 +185,30 @@ class PointEstimator:
 
 def optimize_g(est: PointEstimator, g_prefix, cfg: ControllerConfig) -> float:
     """gopt.py:359-427: bounded Brent on the squared echo distance, grid
-    search fallback."""
+    search fallback.  With ``cfg.prefix_cache`` every evaluation continues
+    from the shared forward states of g_prefix (one period + the echo each)."""
     from scipy.optimize import minimize_scalar
 
-    def objective(gc):
-        return (est(list(g_prefix) + [gc], want_fwd=False)[1] - cfg.target_echo) ** 2
+    use_prefix = bool(cfg.prefix_cache) and len(g_prefix) > 0 and hasattr(est._eng(),
+                                                                          "prefix_build")
+    if use_prefix:
+        est.build_prefix(g_prefix)
+    try:
+        def objective(gc):
+            return (est(list(g_prefix) + [gc], want_fwd=False)[1] - cfg.target_echo) ** 2
 
-    r = minimize_scalar(objective, bounds=(cfg.g_min, cfg.g_max), method="bounded")
-    if r.success:
-        return float(r.x)
-    best, best_d = cfg.g_min, float("inf")
-    for gc in np.linspace(cfg.g_min, cfg.g_max, 10):
-        d = abs(est(list(g_prefix) + [gc], want_fwd=False)[1] - cfg.target_echo)
-        if d < best_d:
-            best, best_d = float(gc), d
-    return best
+        r = minimize_scalar(objective, bounds=(cfg.g_min, cfg.g_max), method="bounded")
+        if r.success:
+            return float(r.x)
+        best, best_d = cfg.g_min, float("inf")
+        for gc in np.linspace(cfg.g_min, cfg.g_max, 10):
+            d = abs(est(list(g_prefix) + [gc], want_fwd=False)[1] - cfg.target_echo)
+            if d < best_d:
+                best, best_d = float(gc), d
+        return best
+    finally:
+        if use_prefix:
+            est.release_prefix()
 
 
 # ---- the realtime loop --------------------------------------------------------------

@@ -46,6 +46,9 @@ def build_parser(script="controlled-g"):
     p.add_argument("--g_max", type=float, default=1.0)
     p.add_argument("--use_optimization", type=int, default=d["use_optimization"])
     p.add_argument("--optimization_iterations", type=int, default=5)
+    p.add_argument("--prefix_cache", type=int, default=1,
+                   help="optimisation: evaluate candidates from the shared t-period forward "
+                        "states (0: a full t+1-period run per evaluation, as the reference)")
     p.add_argument("--shots", type=int, default=1024)
     p.add_argument("--seed", type=int, default=0x5EED0001)
     p.add_argument("--disorder_folder", type=str, default=".")
@@ -62,7 +65,8 @@ def main(argv=None):
         raise SystemExit("--use_optimization belongs to --script g-optimization")
     cfg = ct.ControllerConfig(args.target_echo, args.feedback_gain, args.exponential_feedback,
                               args.decay_compensation, args.g_min, args.g_max,
-                              args.use_optimization, args.optimization_iterations)
+                              args.use_optimization, args.optimization_iterations,
+                              args.prefix_cache)
     L, T = args.L, args.tf
     hs, phis = load_disorder(L, args.inst, args.disorder_folder)
     device = None

@@ -79,6 +79,14 @@ struct dtc_ctx {
   DevBuf recs, recs1, pk;               // kick records (batch schedule / single pass), pass list
   DevBuf dev_thr, dev_jump, dev_kraus;  // device-like noise tables (dtc_autocorr_device)
   std::vector<dtc::PassKick> pk_host;   // staged pass list (alive until the stream syncs)
+  // forward prefix (dtc_prefix_build): every trajectory's state after
+  // prefix_periods periods, and what it was built from
+  DevBuf prefix;
+  std::vector<int64_t> prefix_masks;
+  int prefix_periods = -1;  // -1: none
+  int64_t prefix_states = 0, prefix_traj_offset = 0, prefix_len = 0;
+  int prefix_n_traj = 0, prefix_device = 0;
+  uint64_t prefix_hash = 0;
   bool prof = false;
   int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
   double st_ms[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
@@ -725,6 +733,7 @@ int dtc_close(dtc_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   release(ctx->F);
   release(ctx->E);
+  release(ctx->prefix);
   release(ctx->partial);
   release(ctx->vals_f);
   release(ctx->vals_e);
@@ -848,9 +857,27 @@ int setup_device_noise(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_noi
   return DTC_OK;
 }
 
+// What a prefix must match: the instances' angles and the kick rows of its
+// periods (FNV-1a over the bytes), so a continuation inverts the same periods.
+uint64_t prefix_hash(const dtc_problem* pr, int n_periods) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  mix(&pr->L, sizeof(pr->L));
+  mix(&pr->n_inst, sizeof(pr->n_inst));
+  mix(&pr->n_sub, sizeof(pr->n_sub));
+  mix(&pr->init_mask, sizeof(pr->init_mask));
+  mix(pr->h, sizeof(double) * (size_t)pr->n_inst * pr->L);
+  if (pr->L > 1) mix(pr->phi, sizeof(double) * (size_t)pr->n_inst * (pr->L - 1));
+  mix(pr->kick, sizeof(double) * 8 * (size_t)n_periods * pr->L * pr->n_sub);
+  return h;
+}
+
 int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                   const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset, int32_t n_traj,
-                  double* fwd, double* echo, double* zsite) {
+                  double* fwd, double* echo, double* zsite, bool use_prefix = false) {
   if (!ctx) return fail(DTC_EINVAL, "null ctx");
   DTC_TRY(check_problem(pr, nz));
   if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
@@ -886,6 +913,19 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
 
   // batch size: F (+ E for echo) resident in HBM
   const int64_t S = (int64_t)pr->n_inst * n_traj;
+  // continuation of a prefix: periods 1..n_pre come from dtc_prefix_build
+  const int n_pre = use_prefix ? ctx->prefix_periods : 0;
+  if (use_prefix) {
+    if (ctx->prefix_periods < 0) return fail(DTC_EINVAL, "no prefix built");
+    if (ctx->prefix_states != S || ctx->prefix_n_traj != n_traj ||
+        ctx->prefix_traj_offset != traj_offset || ctx->prefix_len != pl.len ||
+        ctx->prefix_device != (dv ? 1 : 0))
+      return fail(DTC_EINVAL, "prefix built for other trajectories / size / noise kind");
+    if (pr->t_first + pr->t_offset <= n_pre || P <= n_pre)
+      return fail(DTC_EINVAL, "prefixed run must measure only after the prefix's periods");
+    if (prefix_hash(pr, n_pre) != ctx->prefix_hash)
+      return fail(DTC_EINVAL, "problem differs from the prefix's in angles or kick rows");
+  }
   const double per_state = (double)pl.len * 16.0 * (want_e ? 2.0 : 1.0);
   int64_t B = pr->batch;
   if (B <= 0) {
@@ -926,14 +966,19 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     const int nb = (int)std::min<int64_t>(B, S - bs);
     for (int b = 0; b < nb; ++b) {
       const int64_t g = bs + b;
-      masks[b] = (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + g % n_traj));
+      masks[b] = use_prefix ? ctx->prefix_masks[g]
+                            : (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + g % n_traj));
     }
     double2* F = (double2*)ctx->F.p;
     double2* E = (double2*)ctx->E.p;
-    DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
-                           hipMemcpyHostToDevice, ctx->stream));
-    DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
-    DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+    // the first forward pass reads the prefix states (or the basis states in F)
+    const double2* F0 = use_prefix ? (const double2*)ctx->prefix.p + (size_t)bs * pl.len : F;
+    if (!use_prefix) {
+      DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
+                             hipMemcpyHostToDevice, ctx->stream));
+      DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
+      DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+    }
     DTC_HIP(hipMemsetAsync(ctx->vals_f.p, 0, (size_t)nb * T * n_obs_f * sizeof(double),
                            ctx->stream));
     if (want_e)
@@ -943,8 +988,8 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
     // and branch the echo at t off F.  The whole batch schedule is built first.
     std::vector<Launch> sched;
-    if (P > 0) {
-      Chain fw = forward_chain(pl, 1, P, dtc::kStreamForward);
+    if (P > n_pre) {
+      Chain fw = forward_chain(pl, n_pre + 1, P - n_pre, dtc::kStreamForward);
       fw.post_after_d = !rc.device;
       // start on a group without the probe site: every echo chain then ends
       // with its kick-only pass on such a group, which the probe does not need
@@ -955,16 +1000,17 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                                    ? (int)pl.groups.size() : 0);
       while (!fw.done()) {
         PassSpec ps = next_pass(fw);
-        const int p = ps.d_index;
+        const int p = ps.d_index + n_pre;  // the chain counts its own periods
         const int t = p - pr->t_offset;
         const bool closes = ps.diag != dtc::kDiagNone;
         const bool meas = closes && want_f && t >= 0 && t >= pr->t_first;
-        sched.push_back(Launch{ps, F, F, meas ? meas_f : dtc::kMeasNone, 0, n_obs_f,
+        sched.push_back(Launch{ps, sched.empty() ? F0 : F, F, meas ? meas_f : dtc::kMeasNone, 0,
+                               n_obs_f,
                                meas ? (double*)ctx->vals_f.p + (size_t)t * n_obs_f : nullptr,
                                (int64_t)T * n_obs_f});
         if (!closes || !want_e || t < 0 || t < pr->t_first) continue;
         std::vector<int> ahead(pl.groups.size());
-        for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > p;
+        for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > ps.d_index;
         Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
         const double2* src = F;
         const size_t chain0 = sched.size();
@@ -1022,6 +1068,65 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   return DTC_OK;
 }
 
+// Forward prefix: the initial states of all n_inst * n_traj trajectories
+// taken through periods 1..n_periods (post_after_d as the forward chain of
+// autocorr_impl, so no kick is pending) into ctx->prefix, in batches in place.
+int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                      const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                      int32_t n_traj, int32_t n_periods) {
+  if (!ctx) return fail(DTC_EINVAL, "null ctx");
+  DTC_TRY(check_problem(pr, nz));
+  if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
+  if (traj_offset < 0) return fail(DTC_EINVAL, "traj_offset must be >= 0");
+  if (n_periods < 1 || n_periods > pr->T - 1 + pr->t_offset)
+    return fail(DTC_EINVAL, "n_periods must be in [1, T - 1 + t_offset]");
+  DTC_HIP(hipSetDevice(ctx->device));
+  RunCfg rc;
+  rc.prob = pr;
+  rc.pl = make_plan(pr->L);
+  rc.seed = seed;
+  rc.traj_offset = traj_offset;
+  rc.n_traj = n_traj;
+  rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
+  thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  if (dv) DTC_TRY(setup_device_noise(ctx, pr, dv, rc));
+  const Plan& pl = rc.pl;
+  DTC_TRY(upload_tables(ctx, pr, pl));
+  const int64_t S = (int64_t)pr->n_inst * n_traj;
+  ctx->prefix_periods = -1;
+  DTC_TRY(ensure(ctx->prefix, (size_t)S * pl.len * 16));
+  ctx->prefix_masks.resize(S);
+  for (int64_t g = 0; g < S; ++g)
+    ctx->prefix_masks[g] = (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + g % n_traj));
+  const int64_t B = std::min<int64_t>(S, 4096);
+  DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
+  for (int64_t bs = 0; bs < S; bs += B) {
+    const int nb = (int)std::min<int64_t>(B, S - bs);
+    double2* F = (double2*)ctx->prefix.p + (size_t)bs * pl.len;
+    DTC_HIP(hipMemcpyAsync(ctx->basis.p, ctx->prefix_masks.data() + bs, nb * sizeof(int64_t),
+                           hipMemcpyHostToDevice, ctx->stream));
+    DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
+    DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+    Chain fw = forward_chain(pl, 1, n_periods, dtc::kStreamForward);
+    fw.post_after_d = !rc.device;
+    std::vector<Launch> sched;
+    while (!fw.done())
+      sched.push_back(Launch{next_pass(fw), F, F, dtc::kMeasNone, 0, 2, nullptr, 0});
+    DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
+    DTC_HIP(hipStreamSynchronize(ctx->stream));  // the staged pass list is reused
+  }
+  if (ctx->prof) DTC_TRY(resolve_pending(ctx));
+  ctx->prefix_periods = n_periods;
+  ctx->prefix_states = S;
+  ctx->prefix_traj_offset = traj_offset;
+  ctx->prefix_n_traj = n_traj;
+  ctx->prefix_len = pl.len;
+  ctx->prefix_device = dv ? 1 : 0;
+  ctx->prefix_hash = prefix_hash(pr, n_periods);
+  return DTC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1038,6 +1143,32 @@ int dtc_autocorr_device(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_no
   if (!dv) return fail(DTC_EINVAL, "null device noise");
   const dtc_noise nz{0.0, 0, 0};
   return autocorr_impl(ctx, pr, &nz, dv, seed, traj_offset, n_traj, fwd, echo, zsite);
+}
+
+int dtc_prefix_build(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                     const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                     int32_t n_traj, int32_t n_periods) {
+  const dtc_noise none{0.0, 0, 0};
+  if (!dv && !nz) return fail(DTC_EINVAL, "null noise");
+  return prefix_build_impl(ctx, pr, dv ? &none : nz, dv, seed, traj_offset, n_traj, n_periods);
+}
+
+int dtc_autocorr_prefixed(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                          const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                          int32_t n_traj, double* fwd, double* echo) {
+  const dtc_noise none{0.0, 0, 0};
+  if (!dv && !nz) return fail(DTC_EINVAL, "null noise");
+  return autocorr_impl(ctx, pr, dv ? &none : nz, dv, seed, traj_offset, n_traj, fwd, echo,
+                       nullptr, true);
+}
+
+int dtc_prefix_release(dtc_ctx* ctx) {
+  if (!ctx) return fail(DTC_EINVAL, "null ctx");
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  release(ctx->prefix);
+  ctx->prefix_masks.clear();
+  ctx->prefix_periods = -1;
+  return DTC_OK;
 }
 
 int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, uint64_t seed,

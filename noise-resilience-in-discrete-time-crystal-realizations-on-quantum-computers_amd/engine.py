@@ -180,6 +180,42 @@ class DtcEngine:
             out["zsite"] = zs
         return out
 
+    # -- forward prefix cache (dtc_prefix_*; user: control.optimize_g) ------
+    def prefix_build(self, spec: SweepSpec, n_traj: int, n_periods: int,
+                     seed: int = 0x5EED0001, traj_offset: int = 0):
+        """Keep every trajectory's state after periods 1..n_periods on the device."""
+        pr = self._problem(spec)
+        dv = _capi.device_struct(spec.device) if spec.device is not None else None
+        _capi.check(self._lib.dtc_prefix_build(
+            self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)),
+            ctypes.byref(dv) if dv is not None else None, ctypes.c_uint64(seed),
+            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), ctypes.c_int32(n_periods)))
+
+    def autocorr_prefixed(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
+                          traj_offset: int = 0, want_fwd: bool = True, want_echo: bool = True,
+                          t_first: int = 0, batch: int = 0):
+        """``autocorr`` continuing from the prefix (periods after it and every
+        echo drawn from ``seed``); same outputs without ``zsite``."""
+        n_inst, T = spec.n_inst, spec.T
+        fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
+        echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
+        pr = self._problem(spec, want_fwd, want_echo, batch, t_first)
+        dv = _capi.device_struct(spec.device) if spec.device is not None else None
+        _capi.check(self._lib.dtc_autocorr_prefixed(
+            self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)),
+            ctypes.byref(dv) if dv is not None else None, ctypes.c_uint64(seed),
+            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(fwd),
+            _capi.as_dptr(echo)))
+        out = {}
+        if want_fwd:
+            out["fwd"] = fwd
+        if want_echo:
+            out["echo"] = echo
+        return out
+
+    def prefix_release(self):
+        _capi.check(self._lib.dtc_prefix_release(self._ctx))
+
     def apply_periods(self, spec: SweepSpec, state: np.ndarray, first_period: int,
                       n_periods: int, inverse: bool = False, inst: int = 0, traj: int = 0,
                       stream: int = 0, seed: int = 0x5EED0001):
