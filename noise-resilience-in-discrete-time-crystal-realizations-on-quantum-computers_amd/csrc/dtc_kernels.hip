@@ -494,7 +494,10 @@ struct RoundPlan {
 #define DTC_TS(i) ((void)0)
 #endif
 
-template <int SHAPE, int NIBS, int KIND>
+// MC, the measurements compiled in (separate instantiations, so a pass
+// carries only the code it can run): 0 = none or the probe, 1 = any mode
+// (per-site / energy Z), 2 = energy with the in-flight <X> points.
+template <int SHAPE, int NIBS, int KIND, int MC = 0>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
 #ifdef DTC_PHASE_TIMING
@@ -635,8 +638,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
       zr[j] = z;
     }
-    const bool probe_only = A.meas == kMeasProbe;
-    const bool energy = A.meas == kMeasEnergy;
+    const bool probe_only = MC == 0 || A.meas == kMeasProbe;
+    const bool energy = MC > 0 && A.meas == kMeasEnergy;
     auto tile_bit = [&](int site) {
       return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
@@ -655,7 +658,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         z = wave_sum(z);
         if (lane == 0) s_red[wave][1] = z;
       }
-    } else {
+    } else if constexpr (MC > 0) {
       double vec[8];
       vec[0] = ptot;
 #pragma unroll
@@ -692,7 +695,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
         for (int w = 0; w < NW; ++w) acc += s_red[w][ws];
         if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
-      } else {
+      } else if constexpr (MC > 0) {
         // observable t: 0 norm, 1..L Z_{t-1}, L+1.. Z_i Z_i+1 (i = t-1-L)
         const int i0 = t <= A.L_real ? t - 1 : t - 1 - A.L_real;
         const int ns = t == 0 ? 0 : (t <= A.L_real ? 1 : 2);
@@ -759,8 +762,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int q = 0; q < 4; ++q) w2 *= R.d(rec0 + 4 * N + q, 2);
     return w2;
   };
-  const bool x_pre = A.meas == kMeasEnergy && (A.meas_parts & kPartXPre);
-  const bool x_post = A.meas == kMeasEnergy && (A.meas_parts & kPartXPost);
+  const bool x_pre = MC == 2 && (A.meas_parts & kPartXPre);
+  const bool x_post = MC == 2 && (A.meas_parts & kPartXPost);
   using IC2 = std::integral_constant<int, 2>;
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
@@ -867,43 +870,68 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
 
 // Kernel symbols per pass shape so rocprofv3 traces separate them.
 #define DTC_DEFINE_PASS(NAME, SHAPE_EXPR)                                          \
-  template <int NIBS, int KIND>                                                    \
+  template <int NIBS, int KIND, int MC>                                            \
   __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
-    pass_body<SHAPE_EXPR, NIBS, KIND>(A);                                          \
+    pass_body<SHAPE_EXPR, NIBS, KIND, MC>(A);                                      \
   }
 DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
 DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
 #undef DTC_DEFINE_PASS
-template <int NIBS>
+template <int NIBS, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
-  pass_body<kShapeD, NIBS, kKindRX>(A);
+  pass_body<kShapeD, NIBS, kKindRX, MC>(A);
 }
 
-template <int NIBS, int KIND>
+template <int NIBS, int KIND, int MC>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
   switch (shape) {
-    case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
-    case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
-    case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
-    case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND>), grid, block, 0, stream, a); break;
-    case kShapeD: hipLaunchKernelGGL((dtc_diag_pass<NIBS>), grid, block, 0, stream, a); break;
+    case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeD:
+      if constexpr (MC == 2) {
+        return hipErrorInvalidValue;  // no kicks: no X point
+      } else {
+        hipLaunchKernelGGL((dtc_diag_pass<NIBS, MC>), grid, block, 0, stream, a);
+      }
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-template <int NIBS>
-hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, hipStream_t stream) {
+template <int NIBS, int MC>
+hipError_t launch_kind_mc(const PassArgs& a, dim3 grid, int shape, int kind,
+                          hipStream_t stream) {
   switch (kind) {
-    case kKindRX: return launch_shape<NIBS, kKindRX>(a, grid, shape, stream);
-    case kKindRY: return launch_shape<NIBS, kKindRY>(a, grid, shape, stream);
-    case kKindGen: return launch_shape<NIBS, kKindGen>(a, grid, shape, stream);
-    case kKindRXU: return launch_shape<NIBS, kKindRXU>(a, grid, shape, stream);
-    case kKindRYU: return launch_shape<NIBS, kKindRYU>(a, grid, shape, stream);
+    case kKindRX: return launch_shape<NIBS, kKindRX, MC>(a, grid, shape, stream);
+    case kKindRY: return launch_shape<NIBS, kKindRY, MC>(a, grid, shape, stream);
+    case kKindGen: return launch_shape<NIBS, kKindGen, MC>(a, grid, shape, stream);
+    case kKindRXU:
+    case kKindRYU:
+      // device-like noise: no in-flight X (dtc_energy_device measures X by
+      // basis-change passes)
+      if constexpr (MC == 2) {
+        return hipErrorInvalidValue;
+      } else {
+        return kind == kKindRXU ? launch_shape<NIBS, kKindRXU, MC>(a, grid, shape, stream)
+                                : launch_shape<NIBS, kKindRYU, MC>(a, grid, shape, stream);
+      }
     default: return hipErrorInvalidValue;
+  }
+}
+
+template <int NIBS>
+hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, int mc,
+                       hipStream_t stream) {
+  switch (mc) {
+    case 0: return launch_kind_mc<NIBS, 0>(a, grid, shape, kind, stream);
+    case 1: return launch_kind_mc<NIBS, 1>(a, grid, shape, kind, stream);
+    default: return launch_kind_mc<NIBS, 2>(a, grid, shape, kind, stream);
   }
 }
 
@@ -916,10 +944,12 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
   int nibs = 0;
   for (int n = 0; n < 3; ++n)
     if (a.act & (0xF << (4 * n))) nibs |= 1 << n;
+  const bool xm = a.meas == kMeasEnergy && (a.meas_parts & (kPartXPre | kPartXPost));
+  const int mc = (a.meas == kMeasNone || a.meas == kMeasProbe) ? 0 : (xm ? 2 : 1);
   switch (nibs) {
-    case 4: return launch_kind<4>(a, grid, shape, kind, stream);
-    case 6: return launch_kind<6>(a, grid, shape, kind, stream);
-    case 7: return launch_kind<7>(a, grid, shape, kind, stream);
+    case 4: return launch_kind<4>(a, grid, shape, kind, mc, stream);
+    case 6: return launch_kind<6>(a, grid, shape, kind, mc, stream);
+    case 7: return launch_kind<7>(a, grid, shape, kind, mc, stream);
     default: return hipErrorInvalidValue;  // group layouts never produce other sets
   }
 }
