@@ -151,6 +151,13 @@ struct Plan {
 // Site groups: group 0 = sites [0, a0) in a contiguous 4096-amplitude tile;
 // further groups take up to `hi_max` sites each (tile = 12 - a column bits of
 // >= 128-B rows + the group's sites).  Defaults: 11 + 9 for L = 20.
+// Site groups: the low group (tile bits 0..11 = sites 0..a_lo-1) and higher
+// groups of a sites each (tile = a_lo.. column bits 0..c-1 + the group's a
+// sites, c = 12 - a).  Sizes are chosen so that the register nibble the
+// diagonal is applied in never straddles the column boundary c (kernel
+// diag_in: one window-table lookup per amplitude): the low group holds 9..12
+// sites, a higher group 9, 8 or 4 (c = 3, 4, 8).  Fewest groups first, then
+// the largest low group, then the largest higher groups.
 Plan make_plan(int L) {
   Plan pl;
   pl.L = L;
@@ -159,34 +166,36 @@ Plan make_plan(int L) {
   pl.n_tiles = 1 << (pl.L_eff - dtc::kTileBits);
   pl.n_chunks = (pl.L_eff + dtc::kChunkBits - 1) / dtc::kChunkBits;
   pl.diag_stride = (pl.n_chunks + pl.L_eff) * 64;
-  int hi_max = 9;
-  if (const char* e = std::getenv("DTC_HI_SITES")) hi_max = std::max(1, std::min(9, std::atoi(e)));
   if (L <= dtc::kTileBits) {
     // one group; the padding sites L..11 get identity kicks (kernel) so the
     // whole 12-bit tile runs the standard round plan
     pl.groups.push_back(Group{0, 0, (1 << dtc::kTileBits) - 1});
     return pl;
   }
-  const int rem0 = L - dtc::kTileBits;
-  const int n_hi = (rem0 + hi_max - 1) / hi_max;
-  // lo group keeps the rest so the hi groups are as full as allowed
-  int a_lo = L - std::min(rem0 + 0, n_hi * hi_max);
-  a_lo = std::max(a_lo, L - n_hi * hi_max);
-  a_lo = std::min(a_lo, dtc::kTileBits);
-  if (const char* e = std::getenv("DTC_LO_SITES")) {
-    int v = std::atoi(e);
-    if (v >= L - n_hi * hi_max && v <= dtc::kTileBits) a_lo = v;
+  static const int kHi[3] = {9, 8, 4};
+  for (int n_hi = (L - dtc::kTileBits + 8) / 9;; ++n_hi) {
+    for (int a_lo = dtc::kTileBits; a_lo >= 9; --a_lo) {
+      const int need = L - a_lo;
+      // n9 nines, n8 eights, the rest fours
+      for (int n9 = n_hi; n9 >= 0; --n9) {
+        for (int n8 = n_hi - n9; n8 >= 0; --n8) {
+          const int n4 = n_hi - n9 - n8;
+          if (9 * n9 + 8 * n8 + 4 * n4 != need) continue;
+          pl.groups.push_back(Group{0, 0, (1 << a_lo) - 1});
+          int s = a_lo;
+          for (int k = 0; k < 3; ++k) {
+            const int cnt = k == 0 ? n9 : (k == 1 ? n8 : n4);
+            for (int i = 0; i < cnt; ++i) {
+              const int a = kHi[k], c = dtc::kTileBits - a;
+              pl.groups.push_back(Group{c, s, ((1 << a) - 1) << c});
+              s += a;
+            }
+          }
+          return pl;
+        }
+      }
+    }
   }
-  pl.groups.push_back(Group{0, 0, (1 << a_lo) - 1});
-  int s = a_lo, rem = L - a_lo;
-  for (int i = 0; i < n_hi; ++i) {
-    const int a = (rem + (n_hi - i) - 1) / (n_hi - i);
-    const int c = dtc::kTileBits - a;
-    pl.groups.push_back(Group{c, s, ((1 << a) - 1) << c});
-    s += a;
-    rem -= a;
-  }
-  return pl;
 }
 
 // Diagonal factor tables (RZZ even/odd bonds + RZ, fast.py:115-120):
@@ -424,6 +433,15 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   }
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
   const Group& g = rc.pl.groups[ps.group];
+  if (ps.diag != dtc::kDiagNone) {
+    // the kernel's diagonal uses the window table of the register nibble it
+    // is applied in (RoundPlan::d_lay): that nibble must not straddle c
+    const bool n0 = g.act & 0xF, n1 = g.act & 0xF0;
+    const bool pre = shape == dtc::kShapeK || shape == dtc::kShapeKD || shape == dtc::kShapeKDK;
+    const int tb = 4 * (pre ? (n1 ? 1 : (n0 ? 0 : 2)) : 2);
+    if (!(tb >= g.c || tb + 4 <= g.c))
+      return fail(DTC_EINVAL, "internal: diagonal nibble straddles the column bits");
+  }
   A.src = src;
   A.dst = dst;
   A.c = g.c;

@@ -593,22 +593,16 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   auto diag_in = [&](auto lay_tag) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
-    if (g0 >= 0) {
-      // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
-      // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
-      // complex products per amplitude
-      const int w0i = (int)(((x0 << 1) >> g0) & 63);
-      const double2 w0 = s_win[w0i];
-      const double2 pc =
-          cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+    // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
+    // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
+    // complex products per amplitude (the engine's site groups keep the
+    // nibble of layout LAY inside or outside the column bits: g0 >= 0)
+    const int w0i = (int)(((x0 << 1) >> g0) & 63);
+    const double2 w0 = s_win[w0i];
+    const double2 pc =
+        cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
 #pragma unroll
-      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
-    } else {
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r)
-        v[r] = cmul(v[r], cmul(gph, diag_phase(s_chunk, A.n_chunks,
-                                               x0 | M.rel(r << (4 * LAY)))));
-    }
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
   };
   // Observables of the tile: (sum |a|^2, sum z_i |a|^2 for the probe or every
   // site, and in energy mode the bond correlators sum z_i z_i+1 |a|^2).  An
