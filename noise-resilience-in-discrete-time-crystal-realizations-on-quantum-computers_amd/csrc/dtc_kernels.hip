@@ -495,8 +495,8 @@ struct RoundPlan {
 #endif
 
 // MC, the measurements compiled in (separate instantiations, so a pass
-// carries only the code it can run): 0 = none or the probe, 1 = any mode
-// (per-site / energy Z), 2 = energy with the in-flight <X> points.
+// carries only the code it can run): 0 = none, 1 = the probe, 2 = any mode
+// (per-site / energy Z), 3 = energy with the in-flight <X> points.
 template <int SHAPE, int NIBS, int KIND, int MC = 0>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
@@ -632,8 +632,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
       zr[j] = z;
     }
-    const bool probe_only = MC == 0 || A.meas == kMeasProbe;
-    const bool energy = MC > 0 && A.meas == kMeasEnergy;
+    const bool probe_only = MC <= 1 || A.meas == kMeasProbe;
+    const bool energy = MC >= 2 && A.meas == kMeasEnergy;
     auto tile_bit = [&](int site) {
       return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
@@ -652,7 +652,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         z = wave_sum(z);
         if (lane == 0) s_red[wave][1] = z;
       }
-    } else if constexpr (MC > 0) {
+    } else if constexpr (MC >= 2) {
       double vec[8];
       vec[0] = ptot;
 #pragma unroll
@@ -689,7 +689,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
         for (int w = 0; w < NW; ++w) acc += s_red[w][ws];
         if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
-      } else if constexpr (MC > 0) {
+      } else if constexpr (MC >= 2) {
         // observable t: 0 norm, 1..L Z_{t-1}, L+1.. Z_i Z_i+1 (i = t-1-L)
         const int i0 = t <= A.L_real ? t - 1 : t - 1 - A.L_real;
         const int ns = t == 0 ? 0 : (t <= A.L_real ? 1 : 2);
@@ -756,8 +756,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int q = 0; q < 4; ++q) w2 *= R.d(rec0 + 4 * N + q, 2);
     return w2;
   };
-  const bool x_pre = MC == 2 && (A.meas_parts & kPartXPre);
-  const bool x_post = MC == 2 && (A.meas_parts & kPartXPost);
+  const bool x_pre = MC == 3 && (A.meas_parts & kPartXPre);
+  const bool x_post = MC == 3 && (A.meas_parts & kPartXPost);
   using IC2 = std::integral_constant<int, 2>;
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
@@ -795,9 +795,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // ---- diagonal and measurement at d_lay ----
   using DL = std::integral_constant<int, RP::d_lay>;
   if constexpr (RP::diag) diag_in(DL{});
-  if (A.meas != kMeasNone && !A.meas_at_end &&
-      (A.meas != kMeasEnergy || (A.meas_parts & kPartZ)))
-    measure_in(DL{}, inv_w2_mid);  // before the post-kick
+  if constexpr (MC > 0) {
+    if (A.meas != kMeasNone && !A.meas_at_end &&
+        (A.meas != kMeasEnergy || (A.meas_parts & kPartZ)))
+      measure_in(DL{}, inv_w2_mid);  // before the post-kick
+  }
   DTC_TS(4);
   // ---- post-kick rounds: 1 -> 0 -> 2 ----
   // (X before a nibble's post-kick: scale 1 / w_post^2 times prod w^2 of the
@@ -825,7 +827,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   } else {
     exchange<RP::d_lay, 2>(v, s_tile, t);
   }
-  if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{}, 1.0);
+  if constexpr (MC > 0) {
+    if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{}, 1.0);
+  }
   if (x_pre || x_post) {
     // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
     // (0 for sites this pass does not kick)
@@ -887,7 +891,7 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
     case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
     case kShapeD:
-      if constexpr (MC == 2) {
+      if constexpr (MC == 3) {
         return hipErrorInvalidValue;  // no kicks: no X point
       } else {
         hipLaunchKernelGGL((dtc_diag_pass<NIBS, MC>), grid, block, 0, stream, a);
@@ -909,7 +913,7 @@ hipError_t launch_kind_mc(const PassArgs& a, dim3 grid, int shape, int kind,
     case kKindRYU:
       // device-like noise: no in-flight X (dtc_energy_device measures X by
       // basis-change passes)
-      if constexpr (MC == 2) {
+      if constexpr (MC == 3) {
         return hipErrorInvalidValue;
       } else {
         return kind == kKindRXU ? launch_shape<NIBS, kKindRXU, MC>(a, grid, shape, stream)
@@ -925,7 +929,8 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, int mc
   switch (mc) {
     case 0: return launch_kind_mc<NIBS, 0>(a, grid, shape, kind, stream);
     case 1: return launch_kind_mc<NIBS, 1>(a, grid, shape, kind, stream);
-    default: return launch_kind_mc<NIBS, 2>(a, grid, shape, kind, stream);
+    case 2: return launch_kind_mc<NIBS, 2>(a, grid, shape, kind, stream);
+    default: return launch_kind_mc<NIBS, 3>(a, grid, shape, kind, stream);
   }
 }
 
@@ -939,7 +944,7 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
   for (int n = 0; n < 3; ++n)
     if (a.act & (0xF << (4 * n))) nibs |= 1 << n;
   const bool xm = a.meas == kMeasEnergy && (a.meas_parts & (kPartXPre | kPartXPost));
-  const int mc = (a.meas == kMeasNone || a.meas == kMeasProbe) ? 0 : (xm ? 2 : 1);
+  const int mc = a.meas == kMeasNone ? 0 : (a.meas == kMeasProbe ? 1 : (xm ? 3 : 2));
   switch (nibs) {
     case 4: return launch_kind<4>(a, grid, shape, kind, mc, stream);
     case 6: return launch_kind<6>(a, grid, shape, kind, mc, stream);
