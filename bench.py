@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=256, help="trajectories per step per GPU")
+    ap.add_argument("--strong-total", type=int, default=0,
+                    help="c2/c3 strong scaling: trajectories per step over ALL ranks (split "
+                         "evenly, --batch ignored); 0 = weak scaling, --batch per GPU")
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -165,6 +168,12 @@ def main():
             args.batch = 1024
     eng = pkg.DtcEngine(local_rank)
     B = args.batch
+    if args.strong_total:
+        # SURVEY.md §8(d) scaling report (north_star: >= 6x strong scaling 1 -> 8
+        # GPUs): the same total trajectory count whatever the rank count
+        if args.strong_total % world:
+            raise SystemExit(f"--strong-total {args.strong_total} is not a multiple of {world} ranks")
+        B = args.strong_total // world
     T = args.tf
     per_traj = periods_per_traj(T)
     sums = np.zeros((2, T))
@@ -234,7 +243,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong_total else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
@@ -247,6 +256,7 @@ def main():
                          f"{B} noisy trajectories per step per GPU, forward+echo"),
             "L": args.L, "tf": T, "g": 0.97, "noise_prob": 0.05,
             "trajectories_per_step_per_gpu": B,
+            "trajectories_per_step": world * B,
             "period_applications_per_trajectory": per_traj,
             "parallelism": f"traj-sharded x{world}",
         },
