@@ -29,7 +29,22 @@
 #include "dtc_kernels.h"
 #include "dtc_rng.h"
 
+// Nontemporal tile loads / stores (bit 0 load, bit 1 store), per pass family:
+// A = passes over a full 12-site group (NIBS 7), B = the others.  The tile is
+// touched once per pass, so streaming hints keep it from displacing lines in
+// the caches: same-box A/B on C2 (profiles/r1r_nt_ab.json) 154.1k -> 159.6k
+// periods*inst/s, group-B pass 1.62 -> 1.53 ms, group A unchanged.  -D
+// overrides are for development A/B builds only.
+#ifndef DTC_NT_A
+#define DTC_NT_A 3
+#endif
+#ifndef DTC_NT_B
+#define DTC_NT_B 3
+#endif
+
 namespace dtc {
+
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -500,6 +515,7 @@ struct RoundPlan {
 template <int SHAPE, int NIBS, int KIND, int MC = 0>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
+  constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
 #ifdef DTC_PHASE_TIMING
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
@@ -563,7 +579,14 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     const char* src = (const char*)(A.src + b * A.state_len);
 #pragma unroll
     for (int r = 0; r < kRegs; ++r)
-      v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
+    {
+      if constexpr (kNt & 1) {
+        const d2v w = __builtin_nontemporal_load((const d2v*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs));
+        v[r] = make_double2(w.x, w.y);
+      } else {
+        v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
+      }
+    }
   }
   DTC_TS(1);
   // vmcnt(16) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt/lgkmcnt
@@ -852,7 +875,14 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   char* dst = (char*)(A.dst + b * A.state_len);
 #pragma unroll
   for (int r = 0; r < kRegs; ++r)
-    *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+  {
+    if constexpr (kNt & 2) {
+      d2v w = {v[r].x, v[r].y};
+      __builtin_nontemporal_store(w, (d2v*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs));
+    } else {
+      *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+    }
+  }
 #ifdef DTC_PHASE_TIMING
   DTC_TS(6);
   if (A.dbg_ts && t < 8 && SHAPE == DTC_PHASE_TIMING) {
