@@ -436,9 +436,12 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   if (ps.diag != dtc::kDiagNone) {
     // the kernel's diagonal uses the window table of the register nibble it
     // is applied in (RoundPlan::d_lay): that nibble must not straddle c
-    const bool n0 = g.act & 0xF, n1 = g.act & 0xF0;
+    // (same rule as RoundPlan: load/store layout IO, other high nibble O)
+    const int nibs = ((g.act & 0xF) ? 1 : 0) | ((g.act & 0xF0) ? 2 : 0) | ((g.act & 0xF00) ? 4 : 0);
+    const int io = dtc::io_layout(nibs), o = 3 - io;
+    const bool n0 = nibs & 1, n_o = (nibs >> o) & 1;
     const bool pre = shape == dtc::kShapeK || shape == dtc::kShapeKD || shape == dtc::kShapeKDK;
-    const int tb = 4 * (pre ? (n1 ? 1 : (n0 ? 0 : 2)) : 2);
+    const int tb = 4 * (pre ? (n_o ? o : (n0 ? 0 : io)) : io);
     if (!(tb >= g.c || tb + 4 <= g.c))
       return fail(DTC_EINVAL, "internal: diagonal nibble straddles the column bits");
   }

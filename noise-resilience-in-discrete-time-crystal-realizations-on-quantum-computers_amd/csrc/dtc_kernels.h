@@ -22,6 +22,16 @@ static constexpr int kSlotXPre = 8 * kRedLanes;
 static constexpr int kSlotXPost = kSlotXPre + kTileBits;
 static constexpr int kRedSlots = kSlotXPost + kTileBits;
 
+// Load/store register layout of a pass over the register nibbles `nibs`
+// (bit n = nibble n holds active sites): 1 (threads = tile bits 0..3, 8..11:
+// 256-B row segments per 16 lanes) for the nibble sets in DTC_IO1_NIBS, else 2
+// (threads = tile bits 0..7).  Same-box A/B (profiles/r1s_io_ab.json): the
+// 12-site low group of C2 runs 1.60 -> 1.56 ms from layout 1.
+#ifndef DTC_IO1_NIBS
+#define DTC_IO1_NIBS (1 << 7)
+#endif
+constexpr int io_layout(int nibs) { return ((DTC_IO1_NIBS >> nibs) & 1) ? 1 : 2; }
+
 enum DiagMode { kDiagNone = 0, kDiagFwd = 1, kDiagConj = 2 };
 enum MeasMode {
   kMeasNone = 0,

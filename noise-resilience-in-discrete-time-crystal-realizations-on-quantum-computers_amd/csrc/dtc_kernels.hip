@@ -484,21 +484,24 @@ struct TileMap {
 };
 
 // Compile-time round plan.  NIBS = register nibbles holding active sites
-// (bit n = nibble n).  Pre-kick rounds 2 -> 0 -> 1 (from the coalesced load
-// layout), diagonal + measurement where the pre-kick ends, post-kick rounds
-// 1 -> 0 -> 2, store from layout 2.
+// (bit n = nibble n).  IO = the load/store layout (io_layout), O = 3 - IO the
+// other high nibble.
+// Pre-kick rounds IO -> 0 -> O, diagonal + measurement where the pre-kick
+// ends, post-kick rounds O -> 0 -> IO, store from layout IO.
 template <int NIBS, int SHAPE>
 struct RoundPlan {
-  static constexpr bool n0 = NIBS & 1, n1 = NIBS & 2, n2 = NIBS & 4;
+  static constexpr int IO = io_layout(NIBS);
+  static constexpr int O = 3 - IO;
+  static constexpr bool n0 = NIBS & 1, nIO = (NIBS >> IO) & 1, nO = (NIBS >> O) & 1;
   static constexpr bool pre = SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK;
   static constexpr bool diag =
       SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeD;
   static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK;
-  static constexpr int d_lay = pre ? (n1 ? 1 : (n0 ? 0 : 2)) : 2;
+  static constexpr int d_lay = pre ? (nO ? O : (n0 ? 0 : IO)) : IO;
   // layouts reached by the post rounds
-  static constexpr int p1 = n1 ? 1 : d_lay;
-  static constexpr int p0 = n0 ? 0 : p1;
-  static constexpr int p2 = n2 ? 2 : p0;
+  static constexpr int pO = nO ? O : d_lay;
+  static constexpr int p0 = n0 ? 0 : pO;
+  static constexpr int pIO = nIO ? IO : p0;
 };
 
 // Development-only phase timing (build with -DDTC_PHASE_TIMING): wave 0 of
@@ -572,19 +575,37 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
 
   // ---- the tile (coalesced 16-B loads: uniform 64-bit base + one per-lane
-  // 32-bit byte offset shared by all 16 accesses, L_eff <= 32) ----
-  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
+  // byte offset shared by all 16 accesses).  The offset is 32-bit whenever it
+  // fits: always for layout 2 (thread bits = tile bits 0..7, L_eff <= 32),
+  // for layout 1 (thread bits include tile bits 8..11) while L_eff <= 28 ----
+  const int64_t vofs64 = M.rel(ybase<RP::IO>(t)) << 4;
+  const uint32_t vofs = (uint32_t)vofs64;
+  const bool ofs32 = RP::IO == 2 || A.L_eff <= 28;
+  auto tile_ofs = [&](int r) -> int64_t { return (M.tbase | M.rel(r << (4 * RP::IO))) << 4; };
   double2 v[kRegs];
   {
     const char* src = (const char*)(A.src + b * A.state_len);
+    if (ofs32) {
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r)
-    {
-      if constexpr (kNt & 1) {
-        const d2v w = __builtin_nontemporal_load((const d2v*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs));
-        v[r] = make_double2(w.x, w.y);
-      } else {
-        v[r] = *(const double2*)(src + ((M.tbase | M.rel(r << 8)) << 4) + vofs);
+      for (int r = 0; r < kRegs; ++r) {
+        const char* a = src + tile_ofs(r) + vofs;
+        if constexpr (kNt & 1) {
+          const d2v w = __builtin_nontemporal_load((const d2v*)a);
+          v[r] = make_double2(w.x, w.y);
+        } else {
+          v[r] = *(const double2*)a;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        const char* a = src + tile_ofs(r) + vofs64;
+        if constexpr (kNt & 1) {
+          const d2v w = __builtin_nontemporal_load((const d2v*)a);
+          v[r] = make_double2(w.x, w.y);
+        } else {
+          v[r] = *(const double2*)a;
+        }
       }
     }
   }
@@ -603,7 +624,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
     if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
     // made visible by the first exchange's barrier, or by this one
-    if constexpr (!(RP::pre && (RP::n0 || RP::n1))) __syncthreads();
+    if constexpr (!(RP::pre && (RP::n0 || RP::nO))) __syncthreads();
   }
   DTC_TS(2);
   // global factor of the factored kicks, i^k * w_pre * w_post, applied with
@@ -781,31 +802,30 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   };
   const bool x_pre = MC == 3 && (A.meas_parts & kPartXPre);
   const bool x_post = MC == 3 && (A.meas_parts & kPartXPost);
-  using IC2 = std::integral_constant<int, 2>;
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
   // (X before a nibble's pre-kick: the state is exact times the factored
   // kicks already applied, whose squared scale is 1 / prod w^2)
   using L0 = std::integral_constant<int, 0>;
-  using L1 = std::integral_constant<int, 1>;
-  using L2 = std::integral_constant<int, 2>;
+  using LIO = std::integral_constant<int, RP::IO>;
+  using LO = std::integral_constant<int, RP::O>;
   if constexpr (RP::pre) {
     double sc = 1.0;
-    if constexpr (RP::n2) {
-      if (x_pre) measure_x(L2{}, sc, kSlotXPre);
-      apply_nibble<2, KIND>(v, R, 0);
-      if (x_pre) sc *= nib_w2(2, 0);
+    if constexpr (RP::nIO) {
+      if (x_pre) measure_x(LIO{}, sc, kSlotXPre);
+      apply_nibble<RP::IO, KIND>(v, R, 0);
+      if (x_pre) sc *= nib_w2(RP::IO, 0);
     }
     if constexpr (RP::n0) {
-      exchange<2, 0>(v, s_tile, t);
+      exchange<RP::IO, 0>(v, s_tile, t);
       if (x_pre) measure_x(L0{}, sc, kSlotXPre);
       apply_nibble<0, KIND>(v, R, 0);
       if (x_pre) sc *= nib_w2(0, 0);
     }
-    if constexpr (RP::n1) {
-      exchange<RP::n0 ? 0 : 2, 1>(v, s_tile, t);
-      if (x_pre) measure_x(L1{}, sc, kSlotXPre);
-      apply_nibble<1, KIND>(v, R, 0);
+    if constexpr (RP::nO) {
+      exchange<RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, t);
+      if (x_pre) measure_x(LO{}, sc, kSlotXPre);
+      apply_nibble<RP::O, KIND>(v, R, 0);
     }
   }
   DTC_TS(3);
@@ -829,29 +849,29 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // post nibbles already applied)
   if constexpr (RP::post) {
     double sc = inv_w2_mid;
-    if constexpr (RP::n1) {
-      exchange<RP::d_lay, 1>(v, s_tile, t);
-      if (x_post) measure_x(L1{}, sc, kSlotXPost);
-      apply_nibble<1, KIND>(v, R, kTileBits);
-      if (x_post) sc *= nib_w2(1, kTileBits);
+    if constexpr (RP::nO) {
+      exchange<RP::d_lay, RP::O>(v, s_tile, t);
+      if (x_post) measure_x(LO{}, sc, kSlotXPost);
+      apply_nibble<RP::O, KIND>(v, R, kTileBits);
+      if (x_post) sc *= nib_w2(RP::O, kTileBits);
     }
     if constexpr (RP::n0) {
-      exchange<RP::p1, 0>(v, s_tile, t);
+      exchange<RP::pO, 0>(v, s_tile, t);
       if (x_post) measure_x(L0{}, sc, kSlotXPost);
       apply_nibble<0, KIND>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(0, kTileBits);
     }
-    if constexpr (RP::n2) {
-      exchange<RP::p0, 2>(v, s_tile, t);
-      if (x_post) measure_x(L2{}, sc, kSlotXPost);
-      apply_nibble<2, KIND>(v, R, kTileBits);
+    if constexpr (RP::nIO) {
+      exchange<RP::p0, RP::IO>(v, s_tile, t);
+      if (x_post) measure_x(LIO{}, sc, kSlotXPost);
+      apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
-    exchange<RP::p2, 2>(v, s_tile, t);
+    exchange<RP::pIO, RP::IO>(v, s_tile, t);
   } else {
-    exchange<RP::d_lay, 2>(v, s_tile, t);
+    exchange<RP::d_lay, RP::IO>(v, s_tile, t);
   }
   if constexpr (MC > 0) {
-    if (A.meas != kMeasNone && A.meas_at_end) measure_in(IC2{}, 1.0);
+    if (A.meas != kMeasNone && A.meas_at_end) measure_in(LIO{}, 1.0);
   }
   if (x_pre || x_post) {
     // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
@@ -873,14 +893,27 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   DTC_TS(5);
 
   char* dst = (char*)(A.dst + b * A.state_len);
+  if (ofs32) {
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r)
-  {
-    if constexpr (kNt & 2) {
-      d2v w = {v[r].x, v[r].y};
-      __builtin_nontemporal_store(w, (d2v*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs));
-    } else {
-      *(double2*)(dst + ((M.tbase | M.rel(r << 8)) << 4) + vofs) = v[r];
+    for (int r = 0; r < kRegs; ++r) {
+      char* a = dst + tile_ofs(r) + vofs;
+      if constexpr (kNt & 2) {
+        d2v w = {v[r].x, v[r].y};
+        __builtin_nontemporal_store(w, (d2v*)a);
+      } else {
+        *(double2*)a = v[r];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      char* a = dst + tile_ofs(r) + vofs64;
+      if constexpr (kNt & 2) {
+        d2v w = {v[r].x, v[r].y};
+        __builtin_nontemporal_store(w, (d2v*)a);
+      } else {
+        *(double2*)a = v[r];
+      }
     }
   }
 #ifdef DTC_PHASE_TIMING
