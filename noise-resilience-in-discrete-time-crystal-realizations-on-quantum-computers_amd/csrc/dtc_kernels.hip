@@ -657,6 +657,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // over the wave leaves, in lane m, the vector's sum signed by the lane-bit
   // parity m: every observable is one such entry (lane pattern of its thread
   // bits), summed over the 4 waves with the wave-bit signs.
+  // MC == 1 (probe passes): measure_in only forms each thread's two sums;
+  // the wave reductions, the barrier and the partial write run after the
+  // tile's stores are issued (probe_finish), off the pass's critical path
+  double pm_tot = 0.0, pm_z = 0.0, pm_inv = 1.0;
+  bool pm_on = false;
   auto measure_in = [&](auto lay_tag, double inv_w2) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
@@ -682,17 +687,26 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
     };
     if (probe_only) {
-      const double tot = wave_sum(ptot);
-      if (lane == 0) s_red[wave][0] = tot;
       const int site = A.probe;
       const int tb = tile_bit(site);
+      double z = 0.0;
       if (tb >= 0) {
         const int j = tb - 4 * LAY;
-        double z;
         if (j >= 0 && j < 4)
           z = j == 0 ? zr[0] : (j == 1 ? zr[1] : (j == 2 ? zr[2] : zr[3]));
         else
           z = ((x0 >> site) & 1) ? -ptot : ptot;
+      }
+      if constexpr (MC == 1) {
+        pm_tot = ptot;
+        pm_z = z;
+        pm_inv = inv_w2;
+        pm_on = true;
+        return;
+      }
+      const double tot = wave_sum(ptot);
+      if (lane == 0) s_red[wave][0] = tot;
+      if (tb >= 0) {
         z = wave_sum(z);
         if (lane == 0) s_red[wave][1] = z;
       }
@@ -758,6 +772,26 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         if (neg) acc = -acc;
       }
       acc *= inv_w2;
+      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    }
+  };
+  auto probe_finish = [&]() {
+    const int wave = t >> 6, lane = t & 63;
+    const int site = A.probe;
+    const bool zin = site < c || (site >= s && site < s + kTileBits - c);
+    const double tot = wave_sum(pm_tot);
+    if (lane == 0) s_red[wave][0] = tot;
+    if (zin) {
+      const double z = wave_sum(pm_z);
+      if (lane == 0) s_red[wave][1] = z;
+    }
+    __syncthreads();
+    if (t < 2) {
+      double acc = 0.0;
+      const int ws = (t == 0 || zin) ? t : 0;
+      for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
+      if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
+      acc *= pm_inv;
       A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
     }
   };
@@ -915,6 +949,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         *(double2*)a = v[r];
       }
     }
+  }
+  if constexpr (MC == 1) {
+    if (pm_on) probe_finish();  // workgroup-uniform (A.meas)
   }
 #ifdef DTC_PHASE_TIMING
   DTC_TS(6);
