@@ -577,10 +577,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // ---- the tile (coalesced 16-B loads: uniform 64-bit base + one per-lane
   // byte offset shared by all 16 accesses).  The offset is 32-bit whenever it
   // fits: always for layout 2 (thread bits = tile bits 0..7, L_eff <= 32),
-  // for layout 1 (thread bits include tile bits 8..11) while L_eff <= 28 ----
+  // for layout 1 (thread bits include tile bits 8..11) while tile bit 11's
+  // global bit is <= 27 (the low group at any L; higher groups to L_eff 28) ----
   const int64_t vofs64 = M.rel(ybase<RP::IO>(t)) << 4;
   const uint32_t vofs = (uint32_t)vofs64;
-  const bool ofs32 = RP::IO == 2 || A.L_eff <= 28;
+  const bool ofs32 = RP::IO == 2 || (c > 11 ? 11 : s + 11 - c) <= 27;
   auto tile_ofs = [&](int r) -> int64_t { return (M.tbase | M.rel(r << (4 * RP::IO))) << 4; };
   double2 v[kRegs];
   {
