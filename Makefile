@@ -18,7 +18,7 @@ $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(SRCS) -o $@
 
 $(ORACLE): oracle/dtc_oracle.c
-	$(CC) -O2 -fopenmp -fPIC -shared -std=c11 -Wall $< -o $@ -lm
+	$(CC) -O3 -march=x86-64-v3 -fopenmp -fPIC -shared -std=c11 -Wall $< -o $@ -lm
 
 resource-usage: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage $(SRCS) -o /tmp/dtc_ru.so

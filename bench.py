@@ -10,15 +10,21 @@ trajectory applies 29 forward periods and sum_{t<30} t = 435 inverse periods
 state.  The metric counts those period applications per second over all
 ranks ("Floquet-periods x instances / s").
 
-Multi-GPU: one process per GPU (torchrun), each rank runs its own B
-trajectories per step (independent units, weak scaling, counter-based RNG
-keyed by global trajectory id), and the per-t sums are all-reduced once at
-the end over RCCL.
+Multi-GPU: one process per GPU.  `--gpus N` spawns the N rank processes
+itself when no launcher set WORLD_SIZE (torchrun works too; a WORLD_SIZE that
+differs from --gpus is refused).  By default a step is 1024 trajectories split
+evenly over the ranks (strong scaling, the north_star's 1 -> 8 GPU target;
+--strong-total 0 --batch B gives weak scaling).  Trajectories are independent
+units with counter-based RNG keyed by the global trajectory id, so there is no
+data-path collective: the per-t sums are all-reduced once at the end over
+RCCL.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-"roofline" for the K-D-K pass kernel (kick . RZZ/RZ diagonal . kick; HIP events
-on the engine's stream over the timed region, all passes that apply the diagonal) and "cpu_baseline" = the C
-oracle (oracle/dtc_oracle.c) on this host's cores for a bounded sample.
+"roofline" for the K-D-K pass kernel (kick . RZZ/RZ diagonal . kick; HIP
+events on the engine's stream over the timed region, all passes that apply
+the diagonal; every rank's rate in per_rank_GBps) and "cpu_baseline" = the
+period-fused CPU restatement (oracle/dtc_oracle.c orc_autocorr_fused) on this
+host's usable cores for a bounded sample, with the CPU model.
 """
 from __future__ import annotations
 
@@ -60,26 +66,34 @@ def periods_per_traj(T, t_offset=0):
     return P + echo
 
 
-def cpu_baseline(spec, n_traj, T_sample, threads, t_offset=0):
-    """Time the C oracle (gate-by-gate restatement) on the host cores."""
+def cpu_baseline(spec, n_traj, T_sample, threads=None, t_offset=0):
+    """Time the period-fused CPU restatement (oracle/dtc_oracle.c:
+    orc_autocorr_fused: the same trajectories as the engine, per-site noisy
+    kicks composed once per period, cache-blocked low/high sweeps, split
+    re/im arrays, OpenMP over trajectories) on this host's usable cores."""
     from oracle import c_oracle
 
+    info = host_cpu_info()
+    threads = threads or info["usable_cores"]
     pkg = importlib.import_module(PKG)
     s = pkg.SweepSpec(L=spec.L, T=T_sample, hs=spec.hs, phis=spec.phis, g=spec.g,
                       noise_prob=spec.noise_prob, use_noise=spec.use_noise, t_offset=t_offset)
     t0 = time.perf_counter()
-    c_oracle.autocorr(s, n_traj, seed=0xC0FFEE, n_threads=threads)
+    c_oracle.autocorr_fused(s, n_traj, seed=0xC0FFEE, n_threads=threads)
     dt = time.perf_counter() - t0
     work = n_traj * periods_per_traj(T_sample, t_offset)
     return {
         "value": work / dt,
         "unit": "periods*instances/s",
         "cores": threads,
+        "cpu_model": info["cpu_model"],
+        "host_cpus_in_affinity": info["affinity_cpus"],
+        "cgroup_cpu_quota": info["cgroup_cpu_quota"],
         "kind": "port",
-        "sample": (f"C oracle (oracle/dtc_oracle.c, gate-by-gate statevector, OpenMP over "
-                   f"trajectories): L={spec.L}, g={spec.g}, p={spec.noise_prob}, "
-                   f"{n_traj} trajectories x T={T_sample} fwd+echo = {work} period "
-                   f"applications in {dt:.1f} s"),
+        "sample": (f"period-fused CPU restatement (oracle/dtc_oracle.c orc_autocorr_fused, "
+                   f"OpenMP over trajectories, {threads} threads): L={spec.L}, g={spec.g}, "
+                   f"p={spec.noise_prob}, {n_traj} trajectories x T={T_sample} fwd+echo = "
+                   f"{work} period applications in {dt:.1f} s"),
     }
 
 
@@ -99,21 +113,132 @@ def read_traffic(bytes_per_launch, suffix="_pmc.json"):
     return k["hbm_bytes_per_launch"] * scale, os.path.relpath(files[-1], ROOT)
 
 
-def main():
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``bench.py --gpus N`` without an external launcher: start N rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rendezvous on 127.0.0.1) and wait for them.  Runs before anything touches
+    the GPU (this process never initialises HIP; the ranks are children, not
+    an exec).  Only rank 0 prints the JSON line.  If a rank fails, the others
+    are terminated (they would wait forever at the next collective).  Returns
+    the first non-zero exit code, or 0."""
+    import subprocess
+
+    port = _free_port()
+    base = dict(os.environ)
+    base.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(n),
+                 "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "ROLE_RANK": "0"})
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in alive:
+                    q.terminate()
+        if alive:
+            time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def spawn_selftest(args) -> int:
+    """Rank-side half of the spawn check (tests/test_bench_spawn.py): every
+    rank joins a gloo group, the world size and the ranks are all-reduced,
+    rank 0 prints one JSON line shaped like the bench line.  No GPU work."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):
+        return 3  # test hook: this rank dies before the rendezvous
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([1.0, float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+        dist.barrier()
+    if rank == 0:
+        B = args.strong_total // world if args.strong_total else args.batch
+        print(json.dumps({"metric": "spawn-selftest", "value": float(t[0]), "n_gpus": world,
+                          "rank_sum": float(t[1]),
+                          "scaling": "strong" if args.strong_total else "weak",
+                          "trajectories_per_step_per_gpu": B}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def host_cpu_info() -> dict:
+    """CPU model and the cores this process may use: the affinity set, capped
+    by a cgroup CPU quota when one is set (a GPU box's share of its host)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return {"cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "usable_cores": usable}
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256, help="trajectories per step per GPU")
-    ap.add_argument("--strong-total", type=int, default=0,
-                    help="c2/c3 strong scaling: trajectories per step over ALL ranks (split "
-                         "evenly, --batch ignored); 0 = weak scaling, --batch per GPU")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="trajectories per step per GPU when --strong-total is 0 (weak scaling)")
+    ap.add_argument("--strong-total", type=int, default=1024,
+                    help="c2/c3: trajectories per step over ALL ranks, split evenly (strong "
+                         "scaling, the north_star's 1 -> 8 GPU target; default 1024); 0 = weak "
+                         "scaling with --batch per GPU")
+    ap.add_argument("--spawn-selftest", action="store_true",
+                    help="CPU-only check of the rank spawn path (gloo, no GPU work)")
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-traj", type=int, default=0, help="0 = two per host thread")
-    ap.add_argument("--cpu-tf", type=int, default=10,
-                    help="time points of the CPU sample (about 10 s on 16 host threads)")
+    ap.add_argument("--cpu-tf", type=int, default=14,
+                    help="time points of the CPU sample (about 5-15 s at two trajectories per "
+                         "host thread)")
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "energy", "ctrl"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
                          "device-like noise (stand-in calibration, data/"
@@ -130,7 +255,16 @@ def main():
                     help="ctrl --ctrl-opt: a full t+1-period run per candidate evaluation")
     ap.add_argument("--shard-bits", type=int, default=3, help="c5: log2 of the shard count")
     ap.add_argument("--instances", type=int, default=32, help="c4: instances per step per GPU")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: this process spawns the ranks (before any GPU call)
+        return spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv)
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to report a "
+                         "different GPU count than requested")
+    if args.spawn_selftest:
+        return spawn_selftest(args)
     if args.config == "c4":
         return main_c4(args)
     if args.config == "c5":
@@ -211,6 +345,14 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     autocorr = (acc.cpu().numpy() / (world * args.steps * B))
+    # every rank's K-D-K pass rate (the north_star's per-GPU roofline at N GPUs)
+    my = torch.tensor([stats[0]["total_ms"], float(stats[0]["launches"]), elapsed],
+                      dtype=torch.float64, device="cuda")
+    per_rank = [my]
+    if dist:
+        per_rank = [torch.zeros_like(my) for _ in range(world)]
+        dist.all_gather(per_rank, my)
+    per_rank = [r.cpu().numpy() for r in per_rank]
 
     if rank != 0:
         if dist:
@@ -229,9 +371,8 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not c3:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        ntr = args.cpu_traj or 2 * threads
-        cpu = cpu_baseline(spec, ntr, args.cpu_tf, threads)
+        threads = host_cpu_info()["usable_cores"]
+        cpu = cpu_baseline(spec, args.cpu_traj or 2 * threads, args.cpu_tf, threads)
 
     info = eng.device_info()
     res = {
@@ -253,7 +394,10 @@ def main():
                             "stand-in calibration data/device_standin_L20.json)" if c3 else
                             "depolarizing p=0.05")
                          + f", 1 disorder instance (hs/phis_L{args.L}.csv row 0), "
-                         f"{B} noisy trajectories per step per GPU, forward+echo"),
+                         + (f"{world * B} noisy trajectories per step split over {world} GPU(s) "
+                            f"(strong scaling)" if args.strong_total else
+                            f"{B} noisy trajectories per step per GPU (weak scaling)")
+                         + ", forward+echo"),
             "L": args.L, "tf": T, "g": 0.97, "noise_prob": 0.05,
             "trajectories_per_step_per_gpu": B,
             "trajectories_per_step": world * B,
@@ -275,6 +419,8 @@ def main():
             "algorithmic_bytes_per_launch": launch_bytes,
             "avg_launch_ms": avg_lo * 1e3,
             "launches": lo["launches"],
+            "per_rank_GBps": [launch_bytes / (r[0] / max(1.0, r[1]) / 1e3) / 1e9
+                              if r[1] else None for r in per_rank],
         },
         "kernels": {
             "kdk_pass": {"launches": lo["launches"], "avg_ms": avg_lo * 1e3,
@@ -567,7 +713,7 @@ def _pass_kernels(stats, elapsed):
 
 
 def _host_threads():
-    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    return host_cpu_info()["usable_cores"]
 
 
 def main_energy(args):
@@ -731,4 +877,4 @@ def main_ctrl(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

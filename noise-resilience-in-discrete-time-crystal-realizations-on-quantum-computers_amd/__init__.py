@@ -17,7 +17,7 @@ PACKAGE_NAME = "noise-resilience-in-discrete-time-crystal-realizations-on-quantu
 from . import _capi  # noqa: E402
 from .kicks import kick_table, POLARIZATIONS, rx, ry  # noqa: E402
 from .disorder import load_disorder, generate_disorder, save_disorder_to_csv  # noqa: E402
-from .engine import DtcEngine, SweepSpec, init_mask, N_ANCILLA_NOISY_GATES  # noqa: E402
+from .engine import DtcEngine, SweepSpec, energy_init_mask, init_mask, N_ANCILLA_NOISY_GATES  # noqa: E402
 from . import circuit, aer, sweep, distributed, sharded, energy, envelopes, control  # noqa: E402
 from . import cli, energy_cli, control_cli  # noqa: E402
 from .circuit import QuantumCircuit, transpile_aer_basis  # noqa: E402
@@ -29,7 +29,7 @@ from .sweep import (run_sweep, get_instances, get_single_out,  # noqa: E402
 
 __all__ = [
     "PACKAGE_NAME", "DtcEngine", "SweepSpec", "kick_table", "POLARIZATIONS", "rx", "ry",
-    "load_disorder", "generate_disorder", "save_disorder_to_csv", "init_mask",
+    "load_disorder", "generate_disorder", "save_disorder_to_csv", "init_mask", "energy_init_mask",
     "N_ANCILLA_NOISY_GATES", "QuantumCircuit", "transpile_aer_basis", "AerSimulator",
     "DtcSimulator", "NoiseModel", "depolarizing_error", "run_sweep", "get_instances",
     "get_single_out", "compute_z_expectation", "write_autocorr_csv", "circuit", "aer",

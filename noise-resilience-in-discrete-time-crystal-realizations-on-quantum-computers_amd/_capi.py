@@ -14,6 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
+ABI_VERSION = 5  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
@@ -130,6 +131,12 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                 "`python -c 'import __graft_entry__ as g; g.build()'`)"
             )
         lib = ctypes.CDLL(p)
+        lib.dtc_abi_version.restype = ctypes.c_int32
+        got = int(lib.dtc_abi_version())
+        if got != ABI_VERSION:
+            # a stale library would misread the ctypes structs below
+            raise DtcError(f"{p} has C-ABI version {got}, this package expects {ABI_VERSION} "
+                           "(rebuild with `make`)")
         P = ctypes.POINTER
         lib.dtc_open.argtypes = [ctypes.c_int32, P(ctypes.c_void_p)]
         lib.dtc_close.argtypes = [ctypes.c_void_p]

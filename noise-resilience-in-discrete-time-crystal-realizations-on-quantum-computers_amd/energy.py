@@ -1,8 +1,10 @@
 """Energy observable path: the
 ``autocorr-delta-a-single-qiskit-fast-energy*.py`` family.
 
-The reference builds an L-qubit circuit (no ancilla; optional neel X gates,
-then t periods of fast.py's U_F; energy.py:136-150) and estimates
+The reference builds an L-qubit circuit (no ancilla; optional neel X gates on
+qubits 2, 4, ..., L-1 -- ``energy_spec`` / ``engine.energy_init_mask``, even L
+raises as the reference does -- then t periods of fast.py's U_F;
+energy.py:136-150) and estimates
 ``<H>`` with ``BackendEstimatorV2`` on AerSimulator under the same
 depolarizing model.  ``H`` comes from ``get_hamiltonian`` (energy.py:83-102):
 
@@ -38,7 +40,7 @@ import os
 
 import numpy as np
 
-from .engine import SweepSpec
+from .engine import SweepSpec, energy_init_mask
 
 HAMILTONIAN_TYPES = ("full", "z_only", "zz_only", "x_only", "z_zz")
 ESTIMATOR_SHOTS = int(math.ceil(1.0 / 0.015625 ** 2))  # BackendEstimatorV2 default precision
@@ -130,6 +132,14 @@ def readout_observables(obs: dict, p01, p10) -> dict:
     return out
 
 
+def energy_spec(L, T, hs, phis, g, initial_state="vacuum", **kw) -> SweepSpec:
+    """The energy circuit's sweep: fast.py's periods on L qubits (no ancilla)
+    from the energy scripts' own initial state (``energy_init_mask``: neel =
+    X on sites 2, 4, ..., L-1, even L raises as in the reference)."""
+    return SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
+                     init_mask_value=energy_init_mask(L, initial_state), **kw)
+
+
 def get_instances_energy(spec: SweepSpec, n_traj: int = ESTIMATOR_SHOTS,
                          hamiltonian_types=("full",), seed: int = 0x5EED0001, engine=None,
                          traj_offset: int = 0, readout=None) -> dict:
@@ -181,9 +191,9 @@ def run_energy(L, g, hs, phis, T, nprobs=(0, 0.001, 0.01, 0.1), use_noise=1,
     eff = accumulated_noise(nprobs) if accumulate else [float(p) for p in nprobs]
     res = {}
     for k, (nprob, p_eff) in enumerate(zip(nprobs, eff)):
-        spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
-                         noise_prob=0.0 if calibration is not None else p_eff,
-                         use_noise=1 if calibration is not None else use_noise)
+        spec = energy_spec(L, T, hs, phis, g, initial_state,
+                           noise_prob=0.0 if calibration is not None else p_eff,
+                           use_noise=1 if calibration is not None else use_noise)
         readout = None
         run_seed = seed
         if calibration is not None:
@@ -205,8 +215,8 @@ def run_energy_device(L, g, hs, phis, T, calibration, initial_state="vacuum",
     error on every measured site, mean over instances — NOT divided by L (the
     script saves ``np.mean(energy, axis=0)`` as is).  ``calibration=None``:
     the script with ``--use_fakebackend 0`` (an empty NoiseModel: noiseless)."""
-    spec = SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, initial_state=initial_state,
-                     noise_prob=0.0, use_noise=1 if calibration is not None else 0)
+    spec = energy_spec(L, T, hs, phis, g, initial_state, noise_prob=0.0,
+                       use_noise=1 if calibration is not None else 0)
     readout = None
     if calibration is not None:
         spec.device = calibration.device_noise(L)

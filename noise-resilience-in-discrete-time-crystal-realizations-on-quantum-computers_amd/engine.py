@@ -88,6 +88,29 @@ def init_mask(L: int, initial_state: str) -> int:
     raise ValueError(f"initial_state must be 'vacuum' or 'neel', got {initial_state!r}")
 
 
+def energy_init_mask(L: int, initial_state: str) -> int:
+    """The energy scripts' preparation (autocorr-delta-a-single-qiskit-fast-energy.py:137-141,
+    the same loop in every ``-energy*.py``): ``for i in range(1, L+1): if i % 2 == 0:
+    circ.x(i)`` on ``QuantumCircuit(L)`` -- L qubits, no ancilla, so qubit i IS site i.
+    For odd L that flips sites 2, 4, ..., L-1; for even L the loop reaches
+    ``circ.x(L)`` on an L-qubit circuit and qiskit raises (index out of range), so
+    this raises too.  (The autocorrelator's ``init_mask`` differs: there qubit 0
+    is the ancilla and circuit qubit i is site i-1.)"""
+    if initial_state == "vacuum":
+        return 0
+    if initial_state != "neel":
+        raise ValueError(f"initial_state must be 'vacuum' or 'neel', got {initial_state!r}")
+    m = 0
+    for i in range(1, L + 1):
+        if i % 2 == 0:
+            if i >= L:
+                raise ValueError(
+                    f"neel preparation of the {L}-qubit energy circuit applies X to qubit {i}, "
+                    f"out of range(0, {L}) (the reference's circ.x({i}) raises for even L)")
+            m |= 1 << i
+    return m
+
+
 class DtcEngine:
     """Owns one device context of libdtc_hip.so."""
 

@@ -19,6 +19,7 @@ statevector and a Binomial(S, (1+A)/2) draw, as Aer does for ideal circuits.
 from __future__ import annotations
 
 import os
+import dataclasses
 from dataclasses import dataclass
 
 import numpy as np
@@ -122,11 +123,9 @@ def get_instances(spec: SweepSpec, echo: bool, shots: int | None = 1024, **kw):
 def get_single_out(spec: SweepSpec, inst_number: int, echo: bool, shots: int | None = 1024,
                    **kw):
     """fast.py:217-224 — returns [T] for one instance."""
-    one = SweepSpec(L=spec.L, T=spec.T, hs=spec.hs[inst_number:inst_number + 1],
-                    phis=spec.phis[inst_number:inst_number + 1], kick=spec.kick,
-                    noise_prob=spec.noise_prob, use_noise=spec.use_noise,
-                    t_offset=spec.t_offset, probe_site=spec.probe_site,
-                    initial_state=spec.initial_state, init_mask_value=spec.init_mask_value)
+    # every field carries over (device-like noise, polarization, ...)
+    one = dataclasses.replace(spec, hs=spec.hs[inst_number:inst_number + 1],
+                              phis=spec.phis[inst_number:inst_number + 1])
     return get_instances(one, echo, shots=shots, **kw)[0]
 
 

@@ -69,6 +69,9 @@ def lib():
                                        ctypes.POINTER(OrcDeviceNoise), ctypes.c_uint64,
                                        ctypes.c_int64]
         _lib.orc_init_mask.restype = ctypes.c_int64
+        _lib.orc_autocorr_fused.argtypes = [ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcNoise),
+                                            ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, _dp,
+                                            _dp, ctypes.c_int32]
     return _lib
 
 
@@ -131,6 +134,29 @@ def autocorr(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True, want_e
         out["echo"] = echo
     if want_zsite:
         out["zsite"] = zs
+    return out
+
+
+def autocorr_fused(spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True,
+                   want_echo=True, n_threads=0, t_first=0):
+    """The period-fused CPU restatement (orc_autocorr_fused: same trajectories
+    and outputs as ``autocorr``, depolarizing noise, no zsite) -- bench.py's
+    CPU baseline."""
+    if getattr(spec, "device", None) is not None:
+        raise ValueError("autocorr_fused: depolarizing noise only")
+    n_inst, T = spec.n_inst, spec.T
+    fwd = np.zeros((n_inst, n_traj, T)) if want_fwd else None
+    echo = np.zeros((n_inst, n_traj, T)) if want_echo else None
+    rc = lib().orc_autocorr_fused(ctypes.byref(_problem(spec, want_fwd, want_echo, t_first)),
+                                  ctypes.byref(_noise(spec)), seed, traj_offset, n_traj,
+                                  _ptr(fwd), _ptr(echo), n_threads)
+    if rc != 0:
+        raise RuntimeError(f"orc_autocorr_fused failed: {rc}")
+    out = {}
+    if want_fwd:
+        out["fwd"] = fwd
+    if want_echo:
+        out["echo"] = echo
     return out
 
 

@@ -324,7 +324,7 @@ def statevector_zsite(L, T, hs, phis, kick, init_mask=0, t_offset=0):
 def energy_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", t_offset=0, dev=None):
     """Exact <Z_i>, <Z_i Z_i+1>, <X_i> of the L-qubit energy circuit
     (autocorr-delta-a-single-qiskit-fast-energy.py:136-150: optional neel X
-    gates, then t periods of fast.py's U_F, no ancilla) under the depolarizing
+    gates on qubits 2, 4, .., L-1 (even L raises, as qiskit does), then t periods of fast.py's U_F, no ancilla) under the depolarizing
     channel after every kick gate and prep X, for t = 0..T-1.  ``dev`` (a
     DeviceNoise): the device-like channel instead (p unused), no read-out."""
     N = 1 << L
@@ -332,8 +332,17 @@ def energy_sweep(L, T, hs, phis, kick, p, initial_state="vacuum", t_offset=0, de
     w = np.ones(N)
     if dev is not None:
         p = dev.site_channels()
+    # neel (energy.py:138-141): X on qubit i for i in 1..L with i even, on an
+    # L-qubit circuit whose qubit i is site i; i = L (even L) is out of range
+    neel = set()
+    if initial_state == "neel":
+        for i in range(1, L + 1):
+            if i % 2 == 0:
+                if i >= L:
+                    raise ValueError("neel on an even-L energy circuit: qubit L out of range")
+                neel.add(i)
     for i in range(L):
-        flipped = initial_state == "neel" and (i + 1) % 2 == 0
+        flipped = i in neel
         pi = p[i][2] if dev is not None else p
         pf = (1 - pi / 2) if flipped else 0.0
         b = (x >> i) & 1

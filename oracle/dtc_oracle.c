@@ -454,6 +454,305 @@ int64_t orc_init_mask(const orc_problem* pr, double p, const orc_device_noise* d
   return (int64_t)init_mask(pr, &rng, (uint64_t)traj);
 }
 
+
+/* ---- period-fused CPU restatement (bench.py's cpu_baseline) -------------
+ * The same trajectories, schedule and Philox draws as orc_autocorr, with each
+ * period fused per state instead of gate by gate:
+ *   - per site, the noisy kick of the period is one 2x2 matrix
+ *     M_i = P_n G_n ... P_1 G_1 (forward) or P_n G_1^+ ... P_1 G_n^+ (inverse);
+ *   - the state is kept as split real / imaginary arrays (4-wide FMA spans);
+ *   - sites 0..11 are applied inside 4096-amplitude blocks, sites >= 12 on
+ *     panels of 16 adjacent columns (2^(L-12) rows, copied to a contiguous
+ *     buffer), i.e. two sweeps of the state per period;
+ *   - the RZZ/RZ layer is D(x) = Dlo[x & 4095] * Dhi[x >> 11] (sites 0..11 and
+ *     their bonds | sites >= 12 and the bonds from 11 up), applied in the
+ *     high-site sweep, where <Z_j> is also accumulated.
+ * Results equal orc_autocorr per trajectory to rounding (tests/test_oracle.py). */
+#define FUS_LO 12
+#define FUS_COLS 16
+
+static void mat2_mul(cpx c[4], const cpx a[4], const cpx b[4]) {
+  cpx r[4];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      r[2 * i + j] = cadd(cmul(a[2 * i], b[j]), cmul(a[2 * i + 1], b[2 + j]));
+  memcpy(c, r, sizeof(r));
+}
+
+static void pauli_mat(int pz, cpx m[4]) {
+  static const cpx P[4][4] = {{{1, 0}, {0, 0}, {0, 0}, {1, 0}},
+                              {{0, 0}, {1, 0}, {1, 0}, {0, 0}},
+                              {{0, 0}, {0, -1}, {0, 1}, {0, 0}},
+                              {{1, 0}, {0, 0}, {0, 0}, {-1, 0}}};
+  memcpy(m, P[pz], sizeof(P[pz]));
+}
+
+/* noisy kick matrix of one site: forward period `period` (row period-1) or
+ * the inverse of period `period` drawn at echo step `step` */
+static void fused_site_kick(const orc_problem* pr, const orc_rng* rng, int site, int period,
+                            int inverse, int step, uint64_t traj, uint32_t stream, cpx m[4]) {
+  pauli_mat(0, m);
+  for (int q = 0; q < pr->n_sub; ++q) {
+    cpx g[4], pm[4];
+    kick_gate(pr, period - 1, site, inverse ? pr->n_sub - 1 - q : q, inverse, g);
+    mat2_mul(m, g, m);
+    const int pz = orc_pauli(rng, traj, stream, (uint32_t)(inverse ? step : period),
+                             (uint32_t)site, (uint32_t)q);
+    if (pz) {
+      pauli_mat(pz, pm);
+      mat2_mul(m, pm, m);
+    }
+  }
+}
+
+typedef struct { double* re; double* im; } split;
+
+/* (a[k], b[k]) <- M (a[k], b[k]) for k < n */
+static void bfly_span(double* restrict are, double* restrict aim, double* restrict bre,
+                      double* restrict bim, size_t n, const cpx m[4]) {
+  const double ar = m[0].re, ai = m[0].im, br = m[1].re, bi = m[1].im;
+  const double cr = m[2].re, ci = m[2].im, dr = m[3].re, di = m[3].im;
+  for (size_t k = 0; k < n; ++k) {
+    const double ur = are[k], ui = aim[k], vr = bre[k], vi = bim[k];
+    are[k] = ar * ur - ai * ui + br * vr - bi * vi;
+    aim[k] = ar * ui + ai * ur + br * vi + bi * vr;
+    bre[k] = cr * ur - ci * ui + dr * vr - di * vi;
+    bim[k] = cr * ui + ci * ur + dr * vi + di * vr;
+  }
+}
+
+/* the kick of index bit i over a contiguous span of 2^nb amplitudes */
+static void kick_span(double* re, double* im, int nb, int i, const cpx m[4]) {
+  const size_t bit = (size_t)1 << i, n = (size_t)1 << nb;
+  if (i == 0) {
+    const double ar = m[0].re, ai = m[0].im, br = m[1].re, bi = m[1].im;
+    const double cr = m[2].re, ci = m[2].im, dr = m[3].re, di = m[3].im;
+    for (size_t x = 0; x < n; x += 2) {
+      const double ur = re[x], ui = im[x], vr = re[x + 1], vi = im[x + 1];
+      re[x] = ar * ur - ai * ui + br * vr - bi * vi;
+      im[x] = ar * ui + ai * ur + br * vi + bi * vr;
+      re[x + 1] = cr * ur - ci * ui + dr * vr - di * vi;
+      im[x + 1] = cr * ui + ci * ur + dr * vi + di * vr;
+    }
+    return;
+  }
+  for (size_t x0 = 0; x0 < n; x0 += 2 * bit)
+    bfly_span(re + x0, im + x0, re + x0 + bit, im + x0 + bit, bit, m);
+}
+
+static void diag_span(double* restrict re, double* restrict im, const double* restrict dre,
+                      const double* restrict dim, double sc, size_t n) {
+  for (size_t k = 0; k < n; ++k) {
+    const double ur = re[k], ui = im[k], cr = dre[k], ci = sc * dim[k];
+    re[k] = ur * cr - ui * ci;
+    im[k] = ur * ci + ui * cr;
+  }
+}
+
+typedef struct {
+  int L, lo;
+  double *dlo_re, *dlo_im;   /* [2^lo]                       */
+  double *dhi_re, *dhi_im;   /* [2^(L-lo+1)] (bits 11..L-1)   */
+  double *pre, *pim;         /* panel [rows][FUS_COLS]        */
+  double *rowd_re, *rowd_im; /* diagonal of one panel row     */
+} fused_ws;
+
+static double zsign(size_t x, int j) { return ((x >> j) & 1) ? -1.0 : 1.0; }
+
+static void fused_tables(const orc_problem* pr, int inst, fused_ws* w) {
+  const int L = pr->L, lo = w->lo;
+  const double* h = pr->h + (size_t)inst * L;
+  const double* phi = pr->phi + (size_t)inst * (L > 1 ? L - 1 : 0);
+  for (size_t x = 0; x < ((size_t)1 << lo); ++x) {
+    double a = 0.0;
+    for (int i = 0; i < lo; ++i) a += h[i] * zsign(x, i);
+    for (int i = 0; i + 1 < lo; ++i) a += phi[i] * zsign(x, i) * zsign(x, i + 1);
+    w->dlo_re[x] = cos(-0.5 * a);
+    w->dlo_im[x] = sin(-0.5 * a);
+  }
+  if (L > lo) {
+    for (size_t y = 0; y < ((size_t)1 << (L - lo + 1)); ++y) {
+      const size_t x = y << (lo - 1); /* bits lo-1 .. L-1 */
+      double a = 0.0;
+      for (int i = lo; i < L; ++i) a += h[i] * zsign(x, i);
+      for (int i = lo - 1; i + 1 < L; ++i) a += phi[i] * zsign(x, i) * zsign(x, i + 1);
+      w->dhi_re[y] = cos(-0.5 * a);
+      w->dhi_im[y] = sin(-0.5 * a);
+    }
+  }
+}
+
+static void probe_span(const double* re, const double* im, size_t x0, size_t n, int j,
+                       double* nn, double* zz) {
+  double a = 0.0, b = 0.0;
+  for (size_t k = 0; k < n; ++k) {
+    const double p = re[k] * re[k] + im[k] * im[k];
+    a += p;
+    b += zsign(x0 + k, j) * p;
+  }
+  *nn += a;
+  *zz += b;
+}
+
+/* kicks on sites < lo inside each 2^lo block (+ the whole diagonal and the
+ * probe when L <= lo); sum |a|^2 and z_j |a|^2 of the result when zj */
+static void fused_low(split psi, const fused_ws* w, const cpx (*M)[4], int diag, int conj,
+                      int diag_first, int j, double* norm, double* zj) {
+  const size_t blk = (size_t)1 << w->lo, n = (size_t)1 << w->L;
+  const double sc = conj ? -1.0 : 1.0;
+  double nn = 0.0, zz = 0.0;
+  for (size_t b0 = 0; b0 < n; b0 += blk) {
+    double *re = psi.re + b0, *im = psi.im + b0;
+    if (diag && diag_first) diag_span(re, im, w->dlo_re, w->dlo_im, sc, blk);
+    for (int i = 0; i < w->lo && i < w->L; ++i) kick_span(re, im, w->lo, i, M[i]);
+    if (diag && !diag_first) diag_span(re, im, w->dlo_re, w->dlo_im, sc, blk);
+    if (zj) probe_span(re, im, b0, blk, j, &nn, &zz);
+  }
+  if (zj) { *norm = nn; *zj = zz; }
+}
+
+/* kicks on sites >= lo and the diagonal D or D^* (before the kicks when
+ * diag_first) on panels of FUS_COLS columns; optional probe after both */
+static void fused_high(split psi, const fused_ws* w, const cpx (*M)[4], int conj, int diag_first,
+                       int j, double* norm, double* zj) {
+  const int L = w->L, lo = w->lo, hb = L - lo;
+  const size_t blk = (size_t)1 << lo, rows = (size_t)1 << hb;
+  const double sc = conj ? -1.0 : 1.0;
+  double nn = 0.0, zz = 0.0;
+  double *PR = w->pre, *PI = w->pim;
+  for (size_t c0 = 0; c0 < blk; c0 += FUS_COLS) {
+    for (size_t r = 0; r < rows; ++r) {
+      memcpy(PR + r * FUS_COLS, psi.re + r * blk + c0, sizeof(double) * FUS_COLS);
+      memcpy(PI + r * FUS_COLS, psi.im + r * blk + c0, sizeof(double) * FUS_COLS);
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == (diag_first ? 0 : 1)) {
+        const size_t b11 = (c0 >> (lo - 1)) & 1;
+        for (size_t r = 0; r < rows; ++r) {
+          const double hr = w->dhi_re[(r << 1) | b11], hi = w->dhi_im[(r << 1) | b11];
+          for (int c = 0; c < FUS_COLS; ++c) {
+            w->rowd_re[c] = hr * w->dlo_re[c0 + c] - hi * w->dlo_im[c0 + c];
+            w->rowd_im[c] = hr * w->dlo_im[c0 + c] + hi * w->dlo_re[c0 + c];
+          }
+          diag_span(PR + r * FUS_COLS, PI + r * FUS_COLS, w->rowd_re, w->rowd_im, sc, FUS_COLS);
+        }
+      } else {
+        for (int i = 0; i < hb; ++i) {
+          const size_t bit = (size_t)1 << i;
+          for (size_t r0 = 0; r0 < rows; r0 += 2 * bit)
+            bfly_span(PR + r0 * FUS_COLS, PI + r0 * FUS_COLS, PR + (r0 + bit) * FUS_COLS,
+                      PI + (r0 + bit) * FUS_COLS, bit * FUS_COLS, M[lo + i]);
+        }
+      }
+    }
+    for (size_t r = 0; r < rows; ++r) {
+      memcpy(psi.re + r * blk + c0, PR + r * FUS_COLS, sizeof(double) * FUS_COLS);
+      memcpy(psi.im + r * blk + c0, PI + r * FUS_COLS, sizeof(double) * FUS_COLS);
+      if (zj) probe_span(PR + r * FUS_COLS, PI + r * FUS_COLS, r * blk + c0, FUS_COLS, j, &nn, &zz);
+    }
+  }
+  if (zj) { *norm = nn; *zj = zz; }
+}
+
+int orc_autocorr_fused(const orc_problem* pr, const orc_noise* nz, uint64_t seed,
+                       int64_t traj_offset, int32_t n_traj, double* fwd, double* echo,
+                       int32_t n_threads) {
+  orc_rng rng0;
+  orc_rng_init(&rng0, nz->p, seed);
+  const orc_rng rng = rng0;
+  const double fac = pow(1.0 - nz->p, (double)nz->n_anc);
+  const int L = pr->L, T = pr->T, P = T - 1 + pr->t_offset, j = pr->probe_site;
+  const int lo = L < FUS_LO ? L : FUS_LO;
+  const size_t n = (size_t)1 << L;
+  const int64_t S = (int64_t)pr->n_inst * n_traj;
+  int err = 0;
+  if (L > 40) return -1;
+#ifdef _OPENMP
+  if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel
+#endif
+  {
+    fused_ws w;
+    w.L = L;
+    w.lo = lo;
+    const size_t nlo = (size_t)1 << lo, nhi = (size_t)1 << (L - lo + 1);
+    const size_t npan = (size_t)FUS_COLS << (L - lo);
+    double* pool = (double*)malloc(sizeof(double) * (2 * nlo + 2 * nhi + 2 * npan + 2 * FUS_COLS +
+                                                     (pr->want_echo ? 4 : 2) * n));
+    cpx(*M)[4] = (cpx(*)[4])malloc(sizeof(cpx) * 4 * (size_t)L);
+    int inst_tab = -1;
+    if (!pool || !M) {
+#ifdef _OPENMP
+#pragma omp atomic write
+#endif
+      err = 1;
+    } else {
+      double* q = pool;
+      w.dlo_re = q; q += nlo; w.dlo_im = q; q += nlo;
+      w.dhi_re = q; q += nhi; w.dhi_im = q; q += nhi;
+      w.pre = q; q += npan; w.pim = q; q += npan;
+      w.rowd_re = q; q += FUS_COLS; w.rowd_im = q; q += FUS_COLS;
+      split F = {q, q + n};
+      q += 2 * n;
+      split E = {q, q + n};
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+      for (int64_t g = 0; g < S; ++g) {
+        const int inst = (int)(g / n_traj);
+        const uint64_t traj = (uint64_t)(traj_offset + g % n_traj);
+        if (inst != inst_tab) {
+          fused_tables(pr, inst, &w);
+          inst_tab = inst;
+        }
+        memset(F.re, 0, 2 * n * sizeof(double));
+        const uint64_t m0 = init_mask(pr, &rng, traj);
+        const double zinit = ((m0 >> j) & 1ull) ? -1.0 : 1.0;
+        F.re[m0] = 1.0;
+        for (int p = 0; p <= P; ++p) {
+          const int t = p - pr->t_offset;
+          double nrm = 1.0, zj = zinit;
+          if (p > 0) {
+            for (int i = 0; i < L; ++i) fused_site_kick(pr, &rng, i, p, 0, 0, traj, 0u, M[i]);
+            if (L > lo) {
+              fused_low(F, &w, (const cpx(*)[4])M, 0, 0, 0, j, NULL, NULL);
+              fused_high(F, &w, (const cpx(*)[4])M, 0, 0, j, &nrm, &zj);
+            } else {
+              fused_low(F, &w, (const cpx(*)[4])M, 1, 0, 0, j, &nrm, &zj);
+            }
+          }
+          (void)nrm;
+          if (t < 0 || t < pr->t_first) continue;
+          if (pr->want_fwd) fwd[(size_t)g * T + t] = fac * zinit * zj;
+          if (pr->want_echo) {
+            memcpy(E.re, F.re, 2 * n * sizeof(double));
+            double ez = zinit, en = 1.0;
+            for (int k = 1; k <= p; ++k) {
+              const int pp = p - k + 1;
+              for (int i = 0; i < L; ++i)
+                fused_site_kick(pr, &rng, i, pp, 1, k, traj, (uint32_t)(1 + t), M[i]);
+              const int last = k == p;
+              if (L > lo) {
+                fused_high(E, &w, (const cpx(*)[4])M, 1, 1, j, NULL, NULL);
+                fused_low(E, &w, (const cpx(*)[4])M, 0, 0, 0, j, last ? &en : NULL,
+                          last ? &ez : NULL);
+              } else {
+                fused_low(E, &w, (const cpx(*)[4])M, 1, 1, 1, j, last ? &en : NULL,
+                          last ? &ez : NULL);
+              }
+            }
+            (void)en;
+            echo[(size_t)g * T + t] = fac * zinit * ez;
+          }
+        }
+      }
+    }
+    free(pool);
+    free(M);
+  }
+  return err ? -3 : 0;
+}
+
 /* Exposed for the RNG contract test. */
 int orc_sample_pauli(double p, uint64_t seed, uint64_t traj, uint32_t stream, uint32_t period,
                      uint32_t site, uint32_t sub) {

@@ -152,9 +152,9 @@ def test_energy_oracle_device_trajectories_match_exact(pkg, state):
     from oracle import energy_oracle
 
     rng = np.random.default_rng(21)
-    L, T, n = 4, 5, 3000
+    L, T, n = 5, 5, 3000
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, initial_state=state)
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.93, state)
     spec.device = harsh_device(pkg, L)
     exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, 0.0, initial_state=state,
                                    dev=spec.device)

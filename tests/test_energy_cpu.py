@@ -58,8 +58,7 @@ def test_trajectory_oracle_noiseless_equals_dm(pkg):
     rng = np.random.default_rng(2)
     L, T = 5, 6
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.9, use_noise=0,
-                         initial_state="neel", polarization="xy")
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.9, "neel", use_noise=0, polarization="xy")
     z, zz, x = energy_oracle.trajectory_energy(spec, 0, 0)
     dz, dzz, dx = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, 0.0, "neel")
     assert np.abs(z - dz).max() < 1e-12
@@ -69,9 +68,9 @@ def test_trajectory_oracle_noiseless_equals_dm(pkg):
 
 def test_trajectory_mean_converges_to_dm(pkg):
     rng = np.random.default_rng(3)
-    L, T, p, n = 4, 5, 0.1, 600
+    L, T, p, n = 5, 5, 0.1, 600
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.95, noise_prob=p, initial_state="neel")
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.95, "neel", noise_prob=p)
     acc = [np.zeros((T, L)), np.zeros((T, L - 1)), np.zeros((T, L))]
     sq = [np.zeros_like(a) for a in acc]
     for tr in range(n):
@@ -96,3 +95,47 @@ def test_energy_decomposition(pkg):
          for ht in pkg.energy.HAMILTONIAN_TYPES}
     assert np.allclose(e["full"], e["z_only"] + e["zz_only"] + e["x_only"])
     assert np.allclose(e["z_zz"], e["z_only"] + e["zz_only"])
+
+
+def test_energy_neel_mapping(pkg):
+    """energy.py:138-141 on QuantumCircuit(L): X on qubits 2, 4, ..., L-1 (qubit i is
+    site i, no ancilla) -- not the autocorrelator's ancilla-offset sites 1, 3, ..."""
+    def literal(L):
+        flips = []
+        for i in range(1, L + 1):       # the reference's loop, restated
+            if i % 2 == 0:
+                if not i < L:           # QuantumCircuit(L).x(i) needs 0 <= i < L
+                    raise IndexError(i)
+                flips.append(i)
+        return sum(1 << i for i in flips)
+
+    for L in (1, 3, 5, 7, 9, 21):
+        assert pkg.energy_init_mask(L, "neel") == literal(L)
+    assert pkg.energy_init_mask(5, "neel") == 0b10100
+    assert pkg.energy_init_mask(7, "neel") == 0b1010100
+    assert pkg.init_mask(5, "neel") == 0b01010    # the ancilla circuit's mapping
+    assert pkg.energy_init_mask(6, "vacuum") == 0
+
+
+@pytest.mark.parametrize("L", [2, 4, 6, 20])
+def test_energy_neel_even_L_rejected(pkg, L):
+    """For even L the reference's circ.x(L) is out of range and raises; the
+    energy path and its oracle refuse the same inputs."""
+    rng = np.random.default_rng(L)
+    hs, phis = random_disorder(rng, L)
+    with pytest.raises(ValueError, match="out of range"):
+        pkg.energy.energy_spec(L, 3, hs, phis, 0.97, "neel")
+    with pytest.raises(ValueError):
+        pkg.energy.run_energy(L, 0.97, hs, phis, 3, initial_state="neel", engine=object())
+    with pytest.raises(ValueError):
+        dm_oracle.energy_sweep(L, 3, hs[0], phis[0], np.zeros((2, L, 1, 8)), 0.0, "neel")
+
+
+def test_energy_neel_odd_L_exact(pkg):
+    """Noiseless neel t=0 values of the energy circuit: Z_i = -1 on sites 2, 4, .."""
+    rng = np.random.default_rng(11)
+    L = 7
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.energy.energy_spec(L, 2, hs, phis, 0.9, "neel", use_noise=0)
+    z, zz, x = dm_oracle.energy_sweep(L, 2, hs[0], phis[0], spec.kick, 0.0, "neel")
+    assert list(z[0]) == [1, 1, -1, 1, -1, 1, -1]

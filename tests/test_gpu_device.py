@@ -161,7 +161,7 @@ def test_device_infinite_t1_is_pauli_noise(pkg, engine):
 # ---- energy path under device-like noise (dtc_energy_device) --------------------
 
 @pytest.mark.parametrize("L,T,n_traj,state,pol", [
-    (4, 6, 4, "neel", "x"),
+    (5, 6, 4, "neel", "x"),
     (7, 5, 3, "vacuum", "xy"),
     (13, 4, 2, "neel", "y"),
     (20, 3, 2, "vacuum", "x"),
@@ -171,8 +171,8 @@ def test_device_energy_matches_oracle(pkg, engine, L, T, n_traj, state, pol):
 
     rng = np.random.default_rng(L + 40)
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.92, polarization=pol,
-                         initial_state=state, device=harsh_device(pkg, L))
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.92, state, polarization=pol,
+                                  device=harsh_device(pkg, L))
     got = engine.energy(spec, n_traj, seed=13)
     for tr in range(n_traj):
         z, zz, x = energy_oracle.trajectory_energy(spec, 0, tr, seed=13)
@@ -183,10 +183,9 @@ def test_device_energy_matches_oracle(pkg, engine, L, T, n_traj, state, pol):
 
 def test_device_energy_means_match_exact_dm(pkg, engine):
     rng = np.random.default_rng(5)
-    L, T, n = 4, 6, 8192
+    L, T, n = 5, 6, 8192
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.95, initial_state="neel",
-                         device=harsh_device(pkg, L))
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.95, "neel", device=harsh_device(pkg, L))
     exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, 0.0, initial_state="neel",
                                    dev=spec.device)
     got = engine.energy(spec, n, seed=77, batch=1000)

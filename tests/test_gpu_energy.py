@@ -12,17 +12,19 @@ TOL = 1e-10
 
 
 @pytest.mark.parametrize("L,T,p,state,pol", [
-    (4, 8, 0.05, "neel", "x"),
+    (4, 8, 0.05, "vacuum", "x"),
+    (5, 8, 0.05, "neel", "x"),
+    (7, 6, 0.1, "neel", "circular_left"),
     (7, 6, 0.1, "vacuum", "circular_left"),
-    (12, 5, 0.05, "neel", "xy"),
+    (13, 5, 0.05, "neel", "xy"),
     (14, 5, 0.05, "vacuum", "x"),
     (17, 4, 0.02, "neel", "y"),
 ])
 def test_energy_matches_oracle(pkg, engine, L, T, p, state, pol):
+    """neel = the energy scripts' preparation (sites 2, 4, .., L-1; odd L)."""
     rng = np.random.default_rng(L + 100)
     hs, phis = random_disorder(rng, L, 2)
-    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.94, noise_prob=p, polarization=pol,
-                         initial_state=state)
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.94, state, noise_prob=p, polarization=pol)
     got = engine.energy(spec, 3, seed=21)
     for inst in range(2):
         for tr in range(3):
@@ -32,14 +34,14 @@ def test_energy_matches_oracle(pkg, engine, L, T, p, state, pol):
             assert np.abs(got["x"][inst, tr] - x).max() < TOL
 
 
-@pytest.mark.parametrize("L,state,pol", [(20, "neel", "x"), (24, "vacuum", "y")])
+@pytest.mark.parametrize("L,state,pol", [(21, "neel", "x"), (20, "vacuum", "x"),
+                                         (24, "vacuum", "y")])
 def test_energy_large_matches_oracle(pkg, engine, L, state, pol):
-    """Two site groups (L=20: sites 0-11 | 12-19) and three (L=24): every
+    """Two site groups (L=20/21: sites 0-11 | 12-..) and three (L=24): every
     group's <X_i> comes from a different pass (mid-pass or next-pass entry)."""
     rng = np.random.default_rng(L + 7)
     hs, phis = random_disorder(rng, L)
-    spec = pkg.SweepSpec(L=L, T=3, hs=hs, phis=phis, g=0.93, noise_prob=0.05, polarization=pol,
-                         initial_state=state)
+    spec = pkg.energy.energy_spec(L, 3, hs, phis, 0.93, state, noise_prob=0.05, polarization=pol)
     got = engine.energy(spec, 2, seed=5)
     for tr in range(2):
         z, zz, x = energy_oracle.trajectory_energy(spec, 0, tr, seed=5)
@@ -116,3 +118,19 @@ def test_energy_cli_files(pkg, golden, tmp_path, mode, cols):
         # t = 0: <H>/L of the vacuum = (sum h_i + sum phi_i) / L  (X terms vanish)
         hs, phis = pkg.load_disorder(4, 1, str(dis))
         assert abs(df["energy_p_0"][0] - (hs[0].sum() + phis[0].sum()) / 4) < 1e-12
+
+
+@pytest.mark.parametrize("L", [5, 7])
+def test_energy_neel_mean_vs_density_matrix(pkg, engine, L):
+    """The energy scripts' neel state at odd L: engine trajectory means vs the
+    exact density matrix of the L-qubit energy circuit."""
+    rng = np.random.default_rng(40 + L)
+    T, p, n = 6, 0.08, 4096
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.96, "neel", noise_prob=p)
+    got = engine.energy(spec, n, seed=17)
+    exact = dm_oracle.energy_sweep(L, T, hs[0], phis[0], spec.kick, p, "neel")
+    for k, key in enumerate(("z", "zz", "x")):
+        v = got[key][0]
+        mean, sd = v.mean(axis=0), v.std(axis=0) / np.sqrt(n) + 1e-12
+        assert np.all(np.abs(mean - exact[k]) < 5 * sd), key

@@ -158,3 +158,30 @@ def test_distribution_statistics_L8(pkg, engine):
         z = np.abs(a.mean(axis=0) - exact)[ok] / (sd[ok] / np.sqrt(n))
         assert np.allclose(a.mean(axis=0)[~ok], exact[~ok], atol=1e-12)
         assert z.max() < 4.5, (key, z)
+
+
+def test_noise_sampler_unbiased_high_resolution(pkg, engine):
+    """2^22 trajectories at L=12, T=2 (sub-0.5 % resolution on the sampler).
+
+    t = 1 forward: RX(pi g) then one Pauli draw on the probe site; X or Y flips
+    <Z_j>, so every trajectory's value is +-(1-p)^6 cos(pi g), flipped with
+    probability exactly p/2 (I, Z keep it) -- a binomial count.  Echo t = 1:
+    the mean is (1-p)^8.  A 1 % bias in the Pauli sampler would
+    be ~4 sigma on the flip count and ~15 sigma on the echo."""
+    from scipy import stats
+
+    L, p, g, n = 12, 0.05, 0.97, 1 << 22
+    rng = np.random.default_rng(12)
+    hs, phis = random_disorder(rng, L)
+    spec = pkg.SweepSpec(L=L, T=2, hs=hs, phis=phis, g=g, noise_prob=p)
+    out = engine.autocorr(spec, n, seed=0xB1A5, batch=32768)
+    fwd1, echo1 = out["fwd"][0, :, 1], out["echo"][0, :, 1]
+    base = (1 - p) ** 6 * np.cos(np.pi * g)
+    assert np.abs(np.abs(fwd1) - abs(base)).max() < 1e-12      # every value is +-base
+    flips = int(np.count_nonzero(np.sign(fwd1) != np.sign(base)))
+    pval = stats.binomtest(flips, n, p / 2).pvalue
+    assert pval > 1e-4, (flips / n, p / 2, pval)
+    assert abs(flips / n / (p / 2) - 1) < 0.01                # within 1 % of p/2
+    m, se = echo1.mean(), echo1.std() / np.sqrt(n)
+    assert abs(m - (1 - p) ** 8) < 4.5 * se, (m, (1 - p) ** 8, se)
+    assert se / (1 - p) ** 8 < 5e-4

@@ -225,3 +225,24 @@ def test_blocks_factorise_oracle(pkg):
         ref = c_oracle.autocorr(b, 1, want_echo=False, want_zsite=True)["zsite"]
         assert np.abs(full[..., lo:hi] - ref).max() < 1e-12
         lo = hi
+
+
+@pytest.mark.parametrize("L,T,pol,state,toff,p", [
+    (4, 6, "x", "vacuum", 0, 0.07),
+    (9, 5, "xy", "neel", 1, 0.07),
+    (12, 5, "x", "vacuum", 0, 0.0),
+    (13, 5, "circular_left", "neel", 0, 0.05),
+    (15, 4, "y", "vacuum", 0, 0.1),
+])
+def test_fused_cpu_restatement_matches_gate_oracle(pkg, L, T, pol, state, toff, p):
+    """bench.py's CPU baseline (orc_autocorr_fused: composed per-site kicks,
+    blocked low/high sweeps, table diagonal) runs the same trajectories as the
+    gate-by-gate oracle: equal per trajectory to rounding."""
+    rng = np.random.default_rng(L)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    a = c_oracle.autocorr(spec, 3, seed=5)
+    b = c_oracle.autocorr_fused(spec, 3, seed=5)
+    assert np.abs(a["fwd"] - b["fwd"]).max() < 1e-12
+    assert np.abs(a["echo"] - b["echo"]).max() < 1e-12
