@@ -235,10 +235,10 @@ def main(argv=None):
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-traj", type=int, default=0, help="0 = two per host thread")
-    ap.add_argument("--cpu-tf", type=int, default=14,
-                    help="time points of the CPU sample (about 5-15 s at two trajectories per "
-                         "host thread)")
+    ap.add_argument("--cpu-traj", type=int, default=0, help="0 = four per host thread (c2)")
+    ap.add_argument("--cpu-tf", type=int, default=20,
+                    help="time points of the CPU sample (c2: about 10 s at four trajectories "
+                         "per host thread)")
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "energy", "ctrl"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
                          "device-like noise (stand-in calibration, data/"
@@ -372,7 +372,7 @@ def main(argv=None):
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not c3:
         threads = host_cpu_info()["usable_cores"]
-        cpu = cpu_baseline(spec, args.cpu_traj or 2 * threads, args.cpu_tf, threads)
+        cpu = cpu_baseline(spec, args.cpu_traj or 4 * threads, args.cpu_tf, threads)
 
     info = eng.device_info()
     res = {
@@ -544,8 +544,13 @@ def main_c4(args):
 
 def main_c5(args):
     """one noiseless state, L=34, tf=30, sharded over 8 ranks
-    (32 GiB per GPU), one all-to-all exchange per period (sharded.py).  On one
-    GPU the same driver runs 2^shard_bits virtual ranks (default L=31 there)."""
+    (32 GiB per GPU): per period the pre-exchange kicks run chunk by chunk and
+    each chunk's transfer to its destination rank (RCCL point-to-point over
+    xGMI, side stream) starts while the next chunk is kicked; the fused pass
+    (kicks of the newly local sites, RZZ/RZ, <Z_i>, next kick) follows
+    (sharded.sharded_forward_pipelined).  On one GPU the same driver runs
+    2^shard_bits virtual ranks (default L=31 there; the transfers are device
+    copies)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -559,8 +564,10 @@ def main_c5(args):
         dist.init_process_group("nccl")
     pkg = importlib.import_module(PKG)
     k = args.shard_bits
-    if world > 1 and world != (1 << k):
-        raise SystemExit("c5: world size must be 2^shard_bits")
+    if world > 1:
+        if world & (world - 1):
+            raise SystemExit("c5: the rank count must be a power of two")
+        k = world.bit_length() - 1   # one shard per rank
     L = args.L if args.L != 20 else (34 if world > 1 else 31)
     T = args.tf
     hs, phis = pkg.load_disorder(34, 1, os.path.join(ROOT, "data"))
@@ -569,41 +576,34 @@ def main_c5(args):
     stepper = pkg.sharded.EngineStepper(eng)
     lay = pkg.sharded.initial_layout(L, k, rank * ((1 << k) // world), (1 << k) // world)
     bufs = stepper.alloc(lay)
-    xt = [0.0]
     W = 1 << k
-
-    def exchange(src, dst):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if world == 1:
-            pkg.sharded.virtual_exchange(src, dst, W)
-        else:
-            pkg.sharded.collective_exchange(src, dst)
-        torch.cuda.synchronize()
-        xt[0] += time.perf_counter() - t0
+    xstats = {}
 
     def step():
-        return pkg.sharded.sharded_forward(stepper, spec, k, rank=rank, world=world,
-                                           exchange=exchange, buffers=bufs)
+        return pkg.sharded.sharded_forward_pipelined(stepper, spec, k, rank=rank, world=world,
+                                                     buffers=bufs, stats=xstats)
 
     for _ in range(args.warmup):
         step()
     eng.reset_stats()
     eng.set_profiling(True)
-    xt[0] = 0.0
+    ex_ms = []
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
+        ex_ms += xstats.get("exchange_ms", [])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
     stats = eng.kernel_stats()
-    el = torch.tensor([elapsed, xt[0]], dtype=torch.float64, device="cuda")
+    P = T - 1
+    xch = float(np.sum(ex_ms)) / 1e3
+    el = torch.tensor([elapsed, xch], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed, xch = float(el[0].item()), float(el[1].item())
@@ -611,12 +611,13 @@ def main_c5(args):
         if dist:
             dist.destroy_process_group()
         return
-    P = T - 1
     lo_s, hi_s = stats[0], stats[1]
     by = lo_s["bytes"] + hi_s["bytes"]
     ms = lo_s["total_ms"] + hi_s["total_ms"]
     achieved = by / (ms / 1e3) / 1e9 if ms else 0.0
     shard_bytes = 16.0 * (1 << (L - k)) * lay.n_shards
+    sent = shard_bytes * (W - 1) / W   # per rank per period
+    per_ex = xch / max(1, args.steps * P)
     res = {
         "metric": f"Floquet-periods/sec, one L={L} state sharded over {W} ranks (C5)",
         "value": args.steps * P / elapsed, "unit": "periods/s", "n_gpus": world,
@@ -627,12 +628,18 @@ def main_c5(args):
                                 f"<Z_i(t)> every period, {W} shards "
                                 f"({'virtual, 1 GPU' if world == 1 else 'one per GPU'})"),
                    "L": L, "tf": T, "shards": W, "parallelism": f"state-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "all pass kernels (kick / K-D-K), per-rank shard",
+        "roofline": {"bound": "hbm", "kernel": "all pass kernels (chunk kicks / K-D-K), per-rank shard",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None},
-        "exchange": {"total_s": xch, "per_period_ms": xch / (args.steps * P) * 1e3,
-                     "bytes_per_period_per_rank": shard_bytes * (W - 1) / W,
-                     "kind": "strided device copy" if world == 1 else "RCCL all_to_all_single"},
+        "period_ms": elapsed / (args.steps * P) * 1e3,
+        "pass_ms_per_period": ms / (args.steps * P),
+        "exchange": {"per_period_ms": per_ex * 1e3,
+                     "bytes_per_period_per_rank": sent,
+                     "GBps_per_rank": sent / per_ex / 1e9 if per_ex > 0 else None,
+                     "window": ("side-stream events from the first chunk's transfer to the last "
+                                "one's completion (overlaps the chunk kicks)"),
+                     "kind": ("strided device copy per chunk (virtual ranks)" if world == 1 else
+                              "RCCL point-to-point per chunk over xGMI (isend/irecv pairs)")},
         "pass_time_frac": ms / 1e3 / elapsed,
         "z_t1_mean": float(out["zsite"][1].mean()),
         "kat_cos_pi_g": float(np.cos(np.pi * 0.97)),

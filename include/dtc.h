@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 5
+#define DTC_ABI_VERSION 6
 
 /* error codes */
 #define DTC_OK 0
@@ -191,6 +191,33 @@ int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise
                    const dtc_shard* shard, uint64_t seed, int64_t traj, int32_t inst,
                    int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
                    const double* src, double* dst, double* obs);
+
+/* dtc_shard_step without waiting: everything is enqueued on the ctx's stream
+ * (dtc_get_stream) and obs_dev (device pointer, nullable) receives
+ * [n_shards][1 + n_local] from a device reduction.  The tables of a bit map are
+ * built and uploaded on its first use and cached (a sweep alternates two), so
+ * the host never blocks on the stream.  The sharded sweep driver orders its
+ * exchanges against these steps with events (sharded.py), and reads obs_dev
+ * after its own synchronisation. */
+int dtc_shard_step_async(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                         const dtc_shard* shard, uint64_t seed, int64_t traj, int32_t inst,
+                         int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                         const double* src, double* dst, double* obs_dev);
+
+/* The period-`period` kick on the local bits pre_mask, restricted to chunk
+ * `chunk` of every shard held: the amplitudes whose top chunk_bits local bits
+ * equal `chunk` (in place; asynchronous, ctx stream).  pre_mask must lie below
+ * the chunk bits.  With chunk_bits = n_global this is the part of a period's
+ * pre-exchange kicks that feeds one destination rank, so the sweep driver can
+ * send chunk c while chunk c+1 is kicked (sharded.py). */
+int dtc_shard_kick_chunk(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                         const dtc_shard* shard, uint64_t seed, int64_t traj, int32_t period,
+                         uint64_t pre_mask, int32_t chunk_bits, int32_t chunk, double* state);
+
+/* The ctx's HIP stream (hipStream_t), for ordering host-side collectives
+ * against the asynchronous entry points; and a wait for everything on it. */
+int dtc_get_stream(dtc_ctx* ctx, void** stream);
+int dtc_synchronize(dtc_ctx* ctx);
 
 /* Host-only: the site groups the engine's passes use for an n_bits-bit state
  * (bit masks, one per group; returns the count or a negative error). */

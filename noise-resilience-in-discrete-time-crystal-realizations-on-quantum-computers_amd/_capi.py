@@ -14,7 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
-ABI_VERSION = 5  # DTC_ABI_VERSION of include/dtc.h this binding matches
+ABI_VERSION = 6  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
@@ -37,6 +37,10 @@ EXPORTED_SYMBOLS = (
     "dtc_prefix_build",
     "dtc_autocorr_prefixed",
     "dtc_prefix_release",
+    "dtc_shard_step_async",
+    "dtc_shard_kick_chunk",
+    "dtc_get_stream",
+    "dtc_synchronize",
 )
 
 KERNEL_LO_PASS = 0
@@ -168,6 +172,18 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, _dp,
         ]
+        lib.dtc_shard_step_async.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
+            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ]
+        lib.dtc_shard_kick_chunk.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_void_p,
+        ]
+        lib.dtc_get_stream.argtypes = [ctypes.c_void_p, P(ctypes.c_void_p)]
+        lib.dtc_synchronize.argtypes = [ctypes.c_void_p]
         lib.dtc_energy.argtypes = [
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_int32, _dp, _dp, _dp,

@@ -93,6 +93,15 @@ struct dtc_ctx {
   double st_bytes[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
+  // sharded state (dtc_shard_*): device tables per bit map, cached so that
+  // the asynchronous steps of a sweep never re-upload from host memory
+  struct ShardTables {
+    uint64_t key = 0;
+    DevBuf diag, sitemap;
+  };
+  std::vector<ShardTables> shard_cache;  // most recent last, at most 4
+  DevBuf shard_kick;
+  uint64_t shard_kick_key = 0;
 };
 
 namespace {
@@ -253,6 +262,12 @@ struct RunCfg {
   int noisy;
   uint32_t thr1, thr2, thr3;
   const int* site_of = nullptr;  // device: physical bit -> logical site (shards)
+  // sharded state: the tables live in ctx->shard_cache / shard_kick, and a
+  // chunk pass covers the low L_eff_override bits of states stride_override apart
+  const double2* diag_tab = nullptr;
+  const double2* kick_tab = nullptr;
+  int L_eff_override = 0;
+  int64_t stride_override = 0;
   // device-like noise (dtc_autocorr_device): general non-unitary kicks, no
   // forward pass runs ahead of a branch point (a jump cannot be undone)
   bool device = false;
@@ -315,12 +330,12 @@ PassSpec next_pass(Chain& ch) {
 
 dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   dtc::PassArgs A{};
-  A.state_len = rc.pl.len;
-  A.L_eff = rc.pl.L_eff;
+  A.state_len = rc.stride_override ? rc.stride_override : rc.pl.len;
+  A.L_eff = rc.L_eff_override ? rc.L_eff_override : rc.pl.L_eff;
   A.L_real = rc.pl.L;
   A.batch_start = batch_start;
   A.n_traj = rc.n_traj;
-  A.diag = (const double2*)ctx->diag.p;
+  A.diag = rc.diag_tab ? rc.diag_tab : (const double2*)ctx->diag.p;
   A.n_chunks = rc.pl.n_chunks;
   A.diag_stride = rc.pl.diag_stride;
   A.probe = rc.prob->probe_site;
@@ -337,7 +352,7 @@ dtc::PrepArgs prep_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int
   P.batch_start = batch_start;
   P.n_traj = rc.n_traj;
   P.traj_offset = rc.traj_offset;
-  P.kick = (const double2*)ctx->kick.p;
+  P.kick = rc.kick_tab ? rc.kick_tab : (const double2*)ctx->kick.p;
   P.n_sub = rc.prob->n_sub;
   P.L_kick = rc.prob->L;
   P.L_real = rc.pl.L;
@@ -468,7 +483,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream));
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
-    ctx->pending.push_back(Pending{kernel, e0, e1, 32.0 * (double)A.state_len * batch});
+    ctx->pending.push_back(
+        Pending{kernel, e0, e1, 32.0 * (double)((int64_t)1 << A.L_eff) * batch});
   }
   if (meas_mode != dtc::kMeasNone && meas_out)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
@@ -1508,15 +1524,103 @@ int dtc_shard_set_basis(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz
   return DTC_OK;
 }
 
-int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
-                   const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t inst,
-                   int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
-                   const double* src, double* dst, double* obs) {
-  if (!ctx || !src || !dst) return fail(DTC_EINVAL, "null ctx/src/dst");
+}  // extern "C"
+
+namespace {
+
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+  const unsigned char* c = (const unsigned char*)p;
+  for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  return h;
+}
+
+// Device tables of one shard bit map (effective diagonal per held shard and
+// the bit -> site map) and the logical kick table, built once and cached.
+int shard_tables(dtc_ctx* ctx, const dtc_problem* pr, const dtc_shard* sh, int inst,
+                 const Plan& pl, RunCfg& rc) {
+  const int L = pr->L, nl = sh->n_local, B = sh->n_shards;
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  uint64_t key = 1469598103934665603ull;
+  key = fnv(key, &L, sizeof(L));
+  key = fnv(key, &sh->n_local, sizeof(int32_t) * 4);
+  key = fnv(key, sh->site_of, sizeof(int32_t) * L);
+  key = fnv(key, &inst, sizeof(inst));
+  key = fnv(key, pr->h + (size_t)inst * L, sizeof(double) * L);
+  if (L > 1) key = fnv(key, pr->phi + (size_t)inst * (L - 1), sizeof(double) * (L - 1));
+  auto& cache = ctx->shard_cache;
+  int hit = -1;
+  for (size_t i = 0; i < cache.size(); ++i)
+    if (cache[i].key == key) hit = (int)i;
+  if (hit < 0) {
+    std::vector<double> he((size_t)B * nl), pe((size_t)B * std::max(nl - 1, 1)), ca(B);
+    for (int b = 0; b < B; ++b)
+      shard_chain(pr, sh, inst, sh->first_rank + b, he.data() + (size_t)b * nl,
+                  pe.data() + (size_t)b * std::max(nl - 1, 1), &ca[b]);
+    std::vector<double> dt;
+    build_diag_tables(pl, B, he.data(), pe.data(), dt, ca.data());
+    if (cache.size() >= 4) {
+      DTC_HIP(hipStreamSynchronize(ctx->stream));  // the evicted tables may be in use
+      release(cache.front().diag);
+      release(cache.front().sitemap);
+      cache.erase(cache.begin());
+    }
+    cache.emplace_back();
+    auto& e = cache.back();
+    DTC_TRY(ensure(e.diag, dt.size() * sizeof(double)));
+    DTC_TRY(ensure(e.sitemap, 64 * sizeof(int)));
+    DTC_HIP(hipMemcpy(e.diag.p, dt.data(), dt.size() * sizeof(double), hipMemcpyHostToDevice));
+    DTC_HIP(hipMemcpy(e.sitemap.p, sh->site_of, 64 * sizeof(int), hipMemcpyHostToDevice));
+    e.key = key;
+    hit = (int)cache.size() - 1;
+  }
+  const size_t kb = (size_t)n_rows * L * pr->n_sub * 8 * sizeof(double);
+  uint64_t kkey = fnv(1469598103934665603ull, &kb, sizeof(kb));
+  kkey = fnv(kkey, pr->kick, kb);
+  if (kkey != ctx->shard_kick_key || !ctx->shard_kick.p) {
+    DTC_HIP(hipStreamSynchronize(ctx->stream));  // the previous table may be in use
+    DTC_TRY(ensure(ctx->shard_kick, kb));
+    DTC_HIP(hipMemcpy(ctx->shard_kick.p, pr->kick, kb, hipMemcpyHostToDevice));
+    ctx->shard_kick_key = kkey;
+  }
+  rc.diag_tab = (const double2*)cache[hit].diag.p;
+  rc.site_of = (const int*)cache[hit].sitemap.p;
+  rc.kick_tab = (const double2*)ctx->shard_kick.p;
+  return DTC_OK;
+}
+
+int shard_check_common(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                       const dtc_shard* sh, int64_t traj, int32_t inst) {
+  if (!ctx) return fail(DTC_EINVAL, "null ctx");
   DTC_TRY(check_problem(pr, nz, 64));
   DTC_TRY(check_shard(pr, sh));
   if (inst < 0 || inst >= pr->n_inst) return fail(DTC_EINVAL, "inst out of range");
   if (traj < 0) return fail(DTC_EINVAL, "traj must be >= 0");
+  return DTC_OK;
+}
+
+RunCfg shard_runcfg(const dtc_problem* pr, const dtc_noise* nz, const dtc_shard* sh,
+                    uint64_t seed, int64_t traj) {
+  RunCfg rc;
+  rc.prob = pr;
+  rc.pl = make_plan(sh->n_local);
+  rc.seed = seed;
+  rc.traj_offset = traj;
+  rc.n_traj = 1;  // batch index b = shard b -> diag table b
+  rc.noisy = nz->p > 0.0 ? 1 : 0;
+  rc.row_kind = classify_rows(pr);
+  thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  return rc;
+}
+
+// dtc_shard_step / dtc_shard_step_async: obs is a host array (copied, then
+// the stream is synchronised) or, when obs_on_device, a device array the
+// reduction writes directly (nothing waits).
+int shard_step_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                    const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t inst,
+                    int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                    const double* src, double* dst, double* obs, bool obs_on_device) {
+  if (!src || !dst) return fail(DTC_EINVAL, "null src/dst");
+  DTC_TRY(shard_check_common(ctx, pr, nz, sh, traj, inst));
   const int nl = sh->n_local;
   const uint64_t all = nl >= 64 ? ~0ull : (1ull << nl) - 1;
   if ((pre_mask | post_mask) & ~all) return fail(DTC_EINVAL, "kick mask has non-local bits");
@@ -1527,38 +1631,14 @@ int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   if (post_mask && period + 1 > n_rows) return fail(DTC_EINVAL, "period + 1 outside kick table");
   DTC_HIP(hipSetDevice(ctx->device));
 
-  RunCfg rc;
-  rc.prob = pr;
-  rc.pl = make_plan(nl);
-  rc.seed = seed;
-  rc.traj_offset = traj;
-  rc.n_traj = 1;  // batch index b = shard b -> diag table b
-  rc.noisy = nz->p > 0.0 ? 1 : 0;
-  rc.row_kind = classify_rows(pr);
-  thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
+  RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
   const Plan& pl = rc.pl;
   const int B = sh->n_shards;
-
-  // tables: per-shard effective diagonal, logical kick table, bit -> site map
-  std::vector<double> he((size_t)B * nl), pe((size_t)B * std::max(nl - 1, 1)), ca(B);
-  for (int b = 0; b < B; ++b)
-    shard_chain(pr, sh, inst, sh->first_rank + b, he.data() + (size_t)b * nl,
-                pe.data() + (size_t)b * std::max(nl - 1, 1), &ca[b]);
-  std::vector<double> dt;
-  build_diag_tables(pl, B, he.data(), pe.data(), dt, ca.data());
-  DTC_TRY(ensure(ctx->diag, dt.size() * sizeof(double)));
-  DTC_HIP(hipMemcpyAsync(ctx->diag.p, dt.data(), dt.size() * sizeof(double),
-                         hipMemcpyHostToDevice, ctx->stream));
-  const size_t kb = (size_t)n_rows * pr->L * pr->n_sub * 8 * sizeof(double);
-  DTC_TRY(ensure(ctx->kick, kb));
-  DTC_HIP(hipMemcpyAsync(ctx->kick.p, pr->kick, kb, hipMemcpyHostToDevice, ctx->stream));
-  DTC_TRY(ensure(ctx->sitemap, 64 * sizeof(int)));
-  DTC_HIP(hipMemcpyAsync(ctx->sitemap.p, sh->site_of, 64 * sizeof(int), hipMemcpyHostToDevice,
-                         ctx->stream));
-  rc.site_of = (const int*)ctx->sitemap.p;
+  DTC_TRY(shard_tables(ctx, pr, sh, inst, pl, rc));
   const int n_obs = 1 + nl;
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * n_obs * sizeof(double)));
+  double* meas_out = obs_on_device ? obs : (double*)ctx->vals_f.p;
 
   auto layer = [&](int p, uint64_t mask, const Group& g) {
     dtc::KickDesc k{1, p - 1, dtc::kKickForward, dtc::kStreamForward, (uint32_t)p,
@@ -1605,18 +1685,89 @@ int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     const bool meas = obs && (int)i == meas_idx;
     DTC_TRY(launch_pass_spec(ctx, rc, 0, B, passes[i], i == 0 ? s2 : d2, d2,
                              meas ? dtc::kMeasSites : dtc::kMeasNone, diag ? 0 : 1, n_obs,
-                             meas ? (double*)ctx->vals_f.p : nullptr, n_obs));
+                             meas ? meas_out : nullptr, n_obs));
   }
   if (obs && passes.empty()) {
     // no pass ran: measure with an identity-only kick pass over group 0
     PassSpec ps{0, layer(1, 0, pl.groups[0]), no_kick(), dtc::kDiagNone, 0};
     ps.pre.row = 0;
-    DTC_TRY(launch_pass_spec(ctx, rc, 0, B, ps, d2, d2, dtc::kMeasSites, 1, n_obs,
-                             (double*)ctx->vals_f.p, n_obs));
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, B, ps, d2, d2, dtc::kMeasSites, 1, n_obs, meas_out,
+                             n_obs));
   }
+  if (obs_on_device) return DTC_OK;
   if (obs)
     DTC_HIP(hipMemcpyAsync(obs, ctx->vals_f.p, (size_t)B * n_obs * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->prof) DTC_TRY(resolve_pending(ctx));
+  return DTC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dtc_shard_step(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                   const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t inst,
+                   int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                   const double* src, double* dst, double* obs) {
+  return shard_step_impl(ctx, pr, nz, sh, seed, traj, inst, period, pre_mask, diag, post_mask,
+                         src, dst, obs, false);
+}
+
+int dtc_shard_step_async(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                         const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t inst,
+                         int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
+                         const double* src, double* dst, double* obs_dev) {
+  return shard_step_impl(ctx, pr, nz, sh, seed, traj, inst, period, pre_mask, diag, post_mask,
+                         src, dst, obs_dev, true);
+}
+
+int dtc_shard_kick_chunk(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                         const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t period,
+                         uint64_t pre_mask, int32_t chunk_bits, int32_t chunk, double* state) {
+  if (!state) return fail(DTC_EINVAL, "null state");
+  DTC_TRY(shard_check_common(ctx, pr, nz, sh, traj, 0));
+  const int nl = sh->n_local;
+  if (chunk_bits < 0 || chunk_bits > 16 || nl - chunk_bits < dtc::kTileBits)
+    return fail(DTC_EINVAL, "chunk_bits must leave >= 12 bits per chunk");
+  if (chunk < 0 || chunk >= (1 << chunk_bits)) return fail(DTC_EINVAL, "chunk out of range");
+  const int nsub = nl - chunk_bits;
+  const uint64_t low = (1ull << nsub) - 1;
+  if (pre_mask & ~low) return fail(DTC_EINVAL, "chunk kick mask reaches the chunk bits");
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  if (!pre_mask) return DTC_OK;
+  if (period < 1 || period > n_rows) return fail(DTC_EINVAL, "period outside kick table");
+  DTC_HIP(hipSetDevice(ctx->device));
+  RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
+  const Plan& pl = rc.pl;
+  DTC_TRY(shard_tables(ctx, pr, sh, 0, pl, rc));
+  rc.L_eff_override = nsub;
+  rc.stride_override = (int64_t)1 << nl;
+  double2* base = (double2*)state + ((size_t)chunk << nsub);
+  for (size_t g = 0; g < pl.groups.size(); ++g) {
+    const Group& G = pl.groups[g];
+    const uint64_t gb = group_bits(G);
+    if (!(pre_mask & gb)) continue;
+    if (gb & ~low) return fail(DTC_EINVAL, "a site group of the kick mask reaches the chunk bits");
+    PassSpec ps{(int)g, no_kick(), no_kick(), dtc::kDiagNone, 0};
+    ps.pre = dtc::KickDesc{1, period - 1, dtc::kKickForward, dtc::kStreamForward,
+                           (uint32_t)period, skip_bits(G, pre_mask)};
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, sh->n_shards, ps, base, base, dtc::kMeasNone, 1, 2,
+                             nullptr, 0));
+  }
+  return DTC_OK;
+}
+
+int dtc_get_stream(dtc_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return fail(DTC_EINVAL, "null ctx/stream");
+  *stream = (void*)ctx->stream;
+  return DTC_OK;
+}
+
+int dtc_synchronize(dtc_ctx* ctx) {
+  if (!ctx) return fail(DTC_EINVAL, "null ctx");
+  DTC_HIP(hipSetDevice(ctx->device));
   DTC_HIP(hipStreamSynchronize(ctx->stream));
   if (ctx->prof) DTC_TRY(resolve_pending(ctx));
   return DTC_OK;

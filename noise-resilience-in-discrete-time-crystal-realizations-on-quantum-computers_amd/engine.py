@@ -307,6 +307,39 @@ class DtcEngine:
             ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr), _capi.as_dptr(obs)))
         return obs
 
+    def shard_step_async(self, spec: SweepSpec, shard, period: int, pre_mask: int, diag: bool,
+                         post_mask: int, src_ptr: int, dst_ptr: int, obs_ptr: int | None = None,
+                         seed: int = 0x5EED0001, traj: int = 0, inst: int = 0):
+        """shard_step enqueued on the engine stream without waiting; obs_ptr
+        (device, [n_shards][1 + n_local] doubles) receives the observables."""
+        _capi.check(self._lib.dtc_shard_step_async(
+            self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
+            ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
+            ctypes.c_int32(inst), ctypes.c_int32(period), ctypes.c_uint64(pre_mask),
+            ctypes.c_int32(int(bool(diag))), ctypes.c_uint64(post_mask),
+            ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr),
+            ctypes.c_void_p(obs_ptr) if obs_ptr else None))
+
+    def shard_kick_chunk(self, spec: SweepSpec, shard, period: int, pre_mask: int,
+                         chunk_bits: int, chunk: int, state_ptr: int, seed: int = 0x5EED0001,
+                         traj: int = 0):
+        """K_period on the local bits pre_mask of chunk `chunk` (top chunk_bits
+        local bits) of every shard held, in place, asynchronously."""
+        _capi.check(self._lib.dtc_shard_kick_chunk(
+            self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
+            ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
+            ctypes.c_int32(period), ctypes.c_uint64(pre_mask), ctypes.c_int32(chunk_bits),
+            ctypes.c_int32(chunk), ctypes.c_void_p(state_ptr)))
+
+    def stream_handle(self) -> int:
+        """The engine's hipStream_t (for torch.cuda.ExternalStream)."""
+        h = ctypes.c_void_p()
+        _capi.check(self._lib.dtc_get_stream(self._ctx, ctypes.byref(h)))
+        return int(h.value or 0)
+
+    def synchronize(self):
+        _capi.check(self._lib.dtc_synchronize(self._ctx))
+
     # -- profiling -------------------------------------------------------
     def set_profiling(self, on: bool):
         _capi.check(self._lib.dtc_set_profiling(self._ctx, int(on)))

@@ -147,6 +147,37 @@ class EngineStepper:
 
     def __init__(self, engine):
         self.engine = engine
+        self._stream = None
+
+    # -- asynchronous interface (sharded_forward_pipelined) --------------------
+    def stream(self):
+        """The engine's HIP stream as a torch stream (events order the exchange
+        stream against it; nothing blocks the host)."""
+        import torch
+
+        if self._stream is None:
+            self._stream = torch.cuda.ExternalStream(self.engine.stream_handle())
+        return self._stream
+
+    def kick_chunk(self, spec, layout, seed, traj, period, pre, chunk_bits, chunk, buf):
+        self.engine.shard_kick_chunk(spec, layout.to_c(), period, pre, chunk_bits, chunk,
+                                     buf.data_ptr(), seed, traj)
+
+    def step_async(self, spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
+                   obs_out):
+        self.engine.shard_step_async(spec, layout.to_c(), period, pre, diag, post,
+                                     src.data_ptr(), dst.data_ptr(),
+                                     obs_out.data_ptr() if obs_out is not None else None,
+                                     seed, traj, inst)
+
+    def obs_buffer(self, n_steps, n_shards, n_obs):
+        import torch
+
+        return torch.zeros((n_steps, n_shards, n_obs), dtype=torch.float64,
+                           device=torch.device("cuda", torch.cuda.current_device()))
+
+    def synchronize(self):
+        self.engine.synchronize()
 
     def plan_groups(self, n_bits):
         return _capi.plan_groups(n_bits)
@@ -229,5 +260,168 @@ def sharded_forward(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0, t
             record(t, obs, lay)
         if on_period is not None:
             on_period(p)
+    fac = (1.0 - spec.p) ** N_ANCILLA_NOISY_GATES
+    return {"zsite": zs, "norm": norm, "fwd": fac * zinit * zs[:, spec.probe_site]}
+
+
+# ---- the pipelined sweep (C5 on the GPU node) -----------------------------------------
+
+class _ChunkExchange:
+    """All-to-all of one period as W chunk transfers, each started as soon as
+    its chunk has been kicked.
+
+    Collective (one shard per process): at step i rank r sends its chunk
+    (r + i) mod W to that rank and receives chunk r of rank (r - i) mod W into
+    position (r - i) mod W (step 0: a local copy) -- every rank runs step i at
+    the same time, so the point-to-point pairs always match.  The transfers run
+    on a side stream that waits for the kick of their chunk (an event on the
+    engine stream); the engine stream waits for all of them before the fused
+    pass.  Virtual ranks (one process): chunk c of every shard is copied to
+    shard c on the side stream.  CPU tensors (gloo tests): the same transfers,
+    synchronously."""
+
+    def __init__(self, stepper, W, rank, world, group):
+        import torch
+
+        self.W, self.rank, self.world, self.group = W, rank, world, group
+        self.cuda = hasattr(stepper, "stream")
+        self.eng = stepper.stream() if self.cuda else None
+        self.side = torch.cuda.Stream() if self.cuda else None
+        self.works = []
+        self.t_events = []  # (start, end) per period, side stream
+
+    def order(self):
+        """Chunk kicked at step i: the destination rank of that step."""
+        if self.world == 1:
+            return list(range(self.W))
+        return [(self.rank + i) % self.W for i in range(self.W)]
+
+    def send(self, i, chunk, src, dst):
+        import torch
+        import torch.distributed as dist
+
+        W = self.W
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(self.eng)
+            self.side.wait_event(ev)
+            if i == 0:
+                start = torch.cuda.Event(enable_timing=True)
+                start.record(self.side)
+                self.t_events.append([start, None])
+            ctx = torch.cuda.stream(self.side)
+        else:
+            import contextlib
+
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if self.world == 1:
+                dst.view(W, W, -1)[chunk].copy_(src.view(W, W, -1)[:, chunk])
+                return
+            s_rank = (self.rank - i) % W
+            sv, dv = src.view(W, -1), dst.view(W, -1)
+            if i == 0:
+                dv[self.rank].copy_(sv[self.rank])
+                return
+            ops = [dist.P2POp(dist.isend, torch.view_as_real(sv[chunk]), chunk, self.group),
+                   dist.P2POp(dist.irecv, torch.view_as_real(dv[s_rank]), s_rank, self.group)]
+            reqs = dist.batch_isend_irecv(ops)
+            if self.cuda:
+                self.works.extend(reqs)
+            else:
+                for r in reqs:
+                    r.wait()
+
+    def finish(self):
+        import torch
+
+        if not self.cuda:
+            return
+        with torch.cuda.stream(self.side):
+            for w in self.works:
+                w.wait()  # the side stream waits for the transfers
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(self.side)
+            self.t_events[-1][1] = end
+        self.works = []
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        self.eng.wait_event(ev)
+
+    def exchange_ms(self):
+        return [a.elapsed_time(b) for a, b in self.t_events if b is not None]
+
+
+def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0,
+                              traj: int = 0, seed: int = 0x5EED0001, rank: int = 0,
+                              world: int = 1, group=None, buffers=None, stats=None):
+    """``sharded_forward`` with the exchange overlapped and no host round trip
+    per period (the C5 schedule on the GPU node).
+
+    Per period: the pre-exchange kicks (every local site group except the one
+    holding the top bits, which the previous fused pass already kicked) run
+    chunk by chunk -- chunk c = the amplitudes with top n_global local bits c
+    = what rank c receives -- and each chunk's transfer starts as soon as it is
+    kicked, while the next chunk is kicked; then the fused pass (kick of the
+    newly local sites, RZZ/RZ, measurement, next kick of the top group) runs
+    on the received shard.  The first period also kicks the top group itself
+    (one whole-shard pass) before its chunks.  Observables go to a device
+    array; the host reads them once at the end and joins the ranks with one
+    all-reduce.  Same results as ``sharded_forward``.
+
+    ``stats`` (dict, optional) receives the per-period exchange windows (ms,
+    side-stream events) on the GPU."""
+    import torch
+
+    L, T = spec.L, spec.T
+    W = 1 << n_global
+    if world not in (1, W):
+        raise ValueError("world must be 1 (virtual ranks) or 2^n_global")
+    n_sh = W // world
+    lay = initial_layout(L, n_global, rank * n_sh, n_sh)
+    A, Bf = buffers if buffers is not None else stepper.alloc(lay)
+    nl, top, allb = lay.n_local, lay.top_mask, lay.local_mask
+    groups = stepper.plan_groups(nl)
+    main = next(g for g in groups if (g >> (nl - 1)) & 1)
+    if any(g & top for g in groups if g != main):
+        raise ValueError("the top local bits must all lie in one site group")
+    post_bits = main | top
+    P = T - 1 + spec.t_offset
+    obs = stepper.obs_buffer(P + 1, n_sh, 1 + nl)
+    layouts = [lay]
+    xch = _ChunkExchange(stepper, W, rank, world, group)
+
+    stepper.set_basis(spec, lay, seed, traj, A)
+    stepper.step_async(spec, lay, seed, traj, inst, 1, 0, False, 0, A, A, obs[0])
+    kicked = 0
+    for p in range(1, P + 1):
+        pre = allb & ~kicked
+        if pre & post_bits:
+            # first period: the top group too (its kicks mix the chunks)
+            stepper.step_async(spec, lay, seed, traj, inst, p, pre & post_bits, False, 0, A, A,
+                               None)
+            pre &= ~post_bits
+        for i, c in enumerate(xch.order()):
+            stepper.kick_chunk(spec, lay, seed, traj, p, pre, n_global, c, A)
+            xch.send(i, c, A, Bf)
+        xch.finish()
+        lay = lay.exchanged()
+        post = post_bits if p < P else 0
+        stepper.step_async(spec, lay, seed, traj, inst, p, top, True, post, Bf, A, obs[p])
+        layouts.append(lay)
+        kicked = post
+    stepper.synchronize()
+    o = obs.cpu().numpy() if hasattr(obs, "cpu") else np.asarray(obs)
+    z = np.stack([z_from_obs(layouts[p], o[p]) for p in range(P + 1)])
+    z = _allreduce(z, group)
+    zinit = 1.0 if z[0, 1 + spec.probe_site] >= 0 else -1.0
+    zs = np.zeros((T, L))
+    norm = np.zeros(T)
+    for p in range(P + 1):
+        t = p - spec.t_offset
+        if t >= 0:
+            norm[t], zs[t] = z[p, 0], z[p, 1:]
+    if stats is not None:
+        stats["exchange_ms"] = xch.exchange_ms() if xch.cuda else []
     fac = (1.0 - spec.p) ** N_ANCILLA_NOISY_GATES
     return {"zsite": zs, "norm": norm, "fwd": fac * zinit * zs[:, spec.probe_site]}

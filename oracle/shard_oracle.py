@@ -118,3 +118,33 @@ class NumpyShardStepper:
                 self._apply(psi, nl, q, self._kick(spec, period + 1, layout.site_of[q], seed, traj))
         dst.numpy().reshape(layout.n_shards, -1)[:] = psi
         return obs
+
+    # -- the asynchronous interface of sharded_forward_pipelined (synchronous here) --
+    def kick_chunk(self, spec, layout, seed, traj, period, pre, chunk_bits, chunk, buf):
+        """K_period on the local bits ``pre`` of chunk ``chunk`` (top chunk_bits
+        local bits) of every shard held, in place (dtc_shard_kick_chunk)."""
+        nl = layout.n_local
+        nsub = nl - chunk_bits
+        if pre >> nsub:
+            raise ValueError("chunk kick mask reaches the chunk bits")
+        psi = buf.numpy().reshape(layout.n_shards, -1)
+        sub = psi[:, chunk << nsub:(chunk + 1) << nsub].copy()
+        for q in range(nsub):
+            if (pre >> q) & 1:
+                self._apply(sub, nsub, q, self._kick(spec, period, layout.site_of[q], seed, traj))
+        psi[:, chunk << nsub:(chunk + 1) << nsub] = sub
+
+    def step_async(self, spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
+                   obs_out):
+        obs = self.step(spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
+                        obs_out is not None)
+        if obs_out is not None:
+            obs_out.numpy()[...] = obs
+
+    def obs_buffer(self, n_steps, n_shards, n_obs):
+        import torch
+
+        return torch.zeros((n_steps, n_shards, n_obs), dtype=torch.float64)
+
+    def synchronize(self):
+        pass

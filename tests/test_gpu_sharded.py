@@ -56,3 +56,53 @@ def test_l30_eight_virtual_ranks(pkg, engine, stepper):
     ref = engine.autocorr(spec, 1, want_echo=False, want_zsite=True)
     assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
     assert np.abs(got["zsite"][1] - np.cos(np.pi * 0.97)).max() < 1e-12
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (14, 1, 6, 0.0, "vacuum", "x", 0),
+    (15, 3, 5, 0.05, "neel", "xy", 1),
+    (22, 3, 5, 0.05, "neel", "x", 0),
+    (26, 2, 4, 0.1, "vacuum", "circular_left", 0),
+])
+def test_pipelined_virtual_shards_match_engine(pkg, engine, stepper, L, k, T, p, state, pol,
+                                               toff):
+    """The production C5 driver: per-chunk kicks (dtc_shard_kick_chunk), chunk
+    transfers on a side stream ordered by events, asynchronous fused steps with
+    device observables (dtc_shard_step_async) -- same values as dtc_autocorr."""
+    rng = np.random.default_rng(L * 11 + k)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    one = dataclasses.replace(spec, hs=hs[1:2], phis=phis[1:2])
+    for traj in (0, 5):
+        got = pkg.sharded.sharded_forward_pipelined(stepper, spec, k, inst=1, traj=traj, seed=77)
+        ref = engine.autocorr(one, 1, seed=77, traj_offset=traj, want_echo=False,
+                              want_zsite=True)
+        assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+        assert np.abs(got["fwd"] - ref["fwd"][0, 0]).max() < TOL
+        assert np.abs(got["norm"] - 1.0).max() < 1e-10
+
+
+def test_l32_eight_virtual_ranks_pipelined(pkg, engine, stepper):
+    """C5's layout at L=32 (8 shards of 2^29, 64 GiB in all) against the
+    whole-state engine at L=32 (64 GiB): the high site groups' 64-bit lane
+    offsets on both sides (dtc_kernels.hip pass_body, ofs32 false) and the
+    chunked pipeline at its largest single-GPU size."""
+    import os
+
+    import torch
+
+    L = 32
+    hs, phis = pkg.load_disorder(34, 1, os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "data"))
+    spec = pkg.SweepSpec(L=L, T=3, hs=hs, phis=phis, g=0.97, use_noise=0)
+    lay = pkg.sharded.initial_layout(L, 3, 0, 8)
+    bufs = stepper.alloc(lay)
+    got = pkg.sharded.sharded_forward_pipelined(stepper, spec, 3, buffers=bufs)
+    del bufs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    ref = engine.autocorr(spec, 1, want_echo=False, want_zsite=True)
+    assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+    assert np.abs(got["zsite"][1] - np.cos(np.pi * 0.97)).max() < 1e-12
+    assert np.abs(got["norm"] - 1.0).max() < 1e-10

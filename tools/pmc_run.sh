@@ -10,6 +10,6 @@ cd /tmp
 i=0
 for set in "$@"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $set -T --output-format csv -d $O -o p$i -- python $R/bench.py --steps 1 --warmup 0 --batch 64 --no-cpu-baseline > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
+  timeout -k 10 240 rocprofv3 --pmc $set -T --output-format csv -d $O -o p$i -- python $R/bench.py --steps 1 --warmup 0 --strong-total 0 --batch 64 --no-cpu-baseline > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
 echo done
