@@ -134,6 +134,16 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                 f"HIP extension not built: {p} is missing (run `make` or "
                 "`python -c 'import __graft_entry__ as g; g.build()'`)"
             )
+        # One HIP runtime per process.  The PyTorch wheel ships its own
+        # libamdhip64 (SONAME libamdhip64.so.7) and loads it by path; if this
+        # library were loaded first it would bring in /opt/rocm's copy, and
+        # torch's later device initialisation in the same process fails ("No
+        # HIP GPUs are available").  Importing torch first makes this
+        # library's libamdhip64.so.7 dependency resolve to the loaded copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(p)
         lib.dtc_abi_version.restype = ctypes.c_int32
         got = int(lib.dtc_abi_version())

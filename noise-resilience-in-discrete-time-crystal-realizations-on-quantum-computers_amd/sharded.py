@@ -386,6 +386,7 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     if any(g & top for g in groups if g != main):
         raise ValueError("the top local bits must all lie in one site group")
     post_bits = main | top
+    chunked = nl - n_global >= 12  # a chunk holds at least one 4096-amplitude tile
     P = T - 1 + spec.t_offset
     obs = stepper.obs_buffer(P + 1, n_sh, 1 + nl)
     layouts = [lay]
@@ -396,13 +397,15 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     kicked = 0
     for p in range(1, P + 1):
         pre = allb & ~kicked
-        if pre & post_bits:
-            # first period: the top group too (its kicks mix the chunks)
-            stepper.step_async(spec, lay, seed, traj, inst, p, pre & post_bits, False, 0, A, A,
-                               None)
-            pre &= ~post_bits
+        if pre & post_bits or not chunked:
+            # the first period's top group (its kicks mix the chunks), or every
+            # pre-kick when a chunk is smaller than a tile
+            whole = pre if not chunked else pre & post_bits
+            stepper.step_async(spec, lay, seed, traj, inst, p, whole, False, 0, A, A, None)
+            pre &= ~whole
         for i, c in enumerate(xch.order()):
-            stepper.kick_chunk(spec, lay, seed, traj, p, pre, n_global, c, A)
+            if pre:
+                stepper.kick_chunk(spec, lay, seed, traj, p, pre, n_global, c, A)
             xch.send(i, c, A, Bf)
         xch.finish()
         lay = lay.exchanged()
