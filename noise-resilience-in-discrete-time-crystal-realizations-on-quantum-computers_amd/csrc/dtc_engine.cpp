@@ -448,6 +448,38 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   }
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
   const Group& g = rc.pl.groups[ps.group];
+  A.zx_reg = -1;
+  A.zx_lane = -1;
+  if (meas_mode == dtc::kMeasEnergy) {
+    // the layout the kernel measures Z, ZZ in (RoundPlan::d_lay, or the IO
+    // layout at the end): its one bond between a register bit and a lane bit
+    const int nibs = ((g.act & 0xF) ? 1 : 0) | ((g.act & 0xF0) ? 2 : 0) | ((g.act & 0xF00) ? 4 : 0);
+    const int io = dtc::io_layout(nibs), o = 3 - io;
+    const bool n0 = nibs & 1, n_o = (nibs >> o) & 1;
+    const bool pre = shape == dtc::kShapeK || shape == dtc::kShapeKD || shape == dtc::kShapeKDK;
+    const int lay = meas_at_end ? io : (pre ? (n_o ? o : (n0 ? 0 : io)) : io);
+    auto tile_bit = [&](int site) {
+      return site < g.c ? site : ((site >= g.s && site < g.s + dtc::kTileBits - g.c) ? g.c + site - g.s : -1);
+    };
+    for (int i = 0; i + 1 < rc.pl.L; ++i) {
+      int reg = -1, lane = -1;
+      for (int site : {i, i + 1}) {
+        const int tb = tile_bit(site);
+        if (tb < 0) continue;
+        if (tb >= 4 * lay && tb < 4 * lay + 4) {
+          reg = tb - 4 * lay;
+        } else {
+          const int q = lay == 2 ? tb : (lay == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
+          if (q < 6) lane = q;
+        }
+      }
+      if (reg >= 0 && lane >= 0) {
+        if (A.zx_reg >= 0) return fail(DTC_EINVAL, "internal: two register-lane bonds in one layout");
+        A.zx_reg = reg;
+        A.zx_lane = lane;
+      }
+    }
+  }
   if (ps.diag != dtc::kDiagNone) {
     // the kernel's diagonal uses the window table of the register nibble it
     // is applied in (RoundPlan::d_lay): that nibble must not straddle c

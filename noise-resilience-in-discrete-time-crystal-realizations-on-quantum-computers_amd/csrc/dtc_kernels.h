@@ -157,6 +157,8 @@ struct PassArgs {
   int meas_at_end;         // measure after the post-kick instead of after the diagonal
   int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 4 L_real
   int meas_parts;          // kMeasEnergy: MeasPart bits
+  int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
+                           // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };

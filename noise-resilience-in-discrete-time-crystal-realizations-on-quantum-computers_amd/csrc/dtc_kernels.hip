@@ -456,10 +456,96 @@ __device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chun
   return ph;
 }
 
+// Value of lane (l ^ M) for every lane l, M = 1 .. 32, without LDS: DPP
+// quad permutes (1, 2) and row rotations (4, 8) on the VALU, and gfx950's
+// v_permlane16_swap / v_permlane32_swap (16, 32).  A row rotation by n gives
+// lane l the value of lane ((l - n) mod 16); l ^ 8 is one such rotation, l ^ 4
+// is (l + 4) or (l - 4) by lane bit 2.  permlane{16,32}_swap(x, x) returns
+// (x with its even rows/lower half copied up, x with its odd rows/upper half
+// copied down): the xor partner is the first for lanes with the bit set.
+template <int M>
+__device__ __forceinline__ int xor_lane_b32(int x) {
+  static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor");
+  if constexpr (M == 1) {
+    return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (M == 2) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (M == 8) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (M == 4) {
+    const int up = __builtin_amdgcn_update_dpp(0, x, 0x12C, 0xF, 0xF, false);  // l - 12 = l + 4
+    const int dn = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // l - 4
+    return (__lane_id() & 4) ? dn : up;
+  } else if constexpr (M == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (__lane_id() & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (__lane_id() & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+
+template <int M>
+__device__ __forceinline__ double xor_lane(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = xor_lane_b32<M>((int)(b & 0xffffffffll));
+  const int hi = xor_lane_b32<M>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  x += xor_lane<32>(x);
+  x += xor_lane<16>(x);
+  x += xor_lane<8>(x);
+  x += xor_lane<4>(x);
+  x += xor_lane<2>(x);
+  x += xor_lane<1>(x);
   return x;
+}
+
+// One butterfly stage of a Walsh-Hadamard transform over the wave's lanes:
+// lane l ends with h(l) + h(l ^ M) or h(l ^ M) - h(l) by lane bit M.
+template <int M>
+__device__ __forceinline__ double wht_stage(double h) {
+  const double o = xor_lane<M>(h);
+  return (__lane_id() & M) ? o - h : h + o;
+}
+
+// Sum of NV per-lane vectors over the wave (NV = 4 or 8), halving the vector
+// count per lane at each of the first stages: afterwards every lane of the
+// group of 8 with lane bits (5, 4, 3) = v (NV = 8; NV = 4: bits (5, 4)
+// and every bit-3 value) holds the wave sum of vector v.  NV/2 + NV/4 + ...
+// lane exchanges instead of 6 NV.
+template <int NV>
+__device__ __forceinline__ double wave_sum_multi(const double (&x)[NV]) {
+  const int lane = __lane_id();
+  double a[NV / 2];
+  const bool h5 = lane & 32;
+#pragma unroll
+  for (int m = 0; m < NV / 2; ++m) {
+    const double keep = h5 ? x[NV / 2 + m] : x[m];
+    const double send = h5 ? x[m] : x[NV / 2 + m];
+    a[m] = keep + xor_lane<32>(send);
+  }
+  const bool h4 = lane & 16;
+  double b[NV / 4];
+#pragma unroll
+  for (int m = 0; m < NV / 4; ++m) {
+    const double keep = h4 ? a[NV / 4 + m] : a[m];
+    const double send = h4 ? a[m] : a[NV / 4 + m];
+    b[m] = keep + xor_lane<16>(send);
+  }
+  double c;
+  if constexpr (NV == 8) {
+    const bool h3 = lane & 8;
+    c = (h3 ? b[1] : b[0]) + xor_lane<8>(h3 ? b[0] : b[1]);
+  } else {
+    c = b[0] + xor_lane<8>(b[0]);
+  }
+  c += xor_lane<4>(c);
+  c += xor_lane<2>(c);
+  c += xor_lane<1>(c);
+  return c;
 }
 
 // Lane patterns kept from a wave's Walsh-Hadamard transform (s_red entries):
@@ -712,30 +798,42 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         if (lane == 0) s_red[wave][1] = z;
       }
     } else if constexpr (MC >= 2) {
-      double vec[8];
-      vec[0] = ptot;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) vec[1 + j] = zr[j];
+      // the total: a full 6-stage transform (every lane pattern a site or a
+      // bond on lane bits needs); the register-bit vectors (z of each
+      // register bit, z z of adjacent register bits, and the one bond between
+      // a register bit and a lane bit, host-chosen: A.zx_reg / A.zx_lane)
+      // need only their wave sums: one multi-vector reduction
+      double h = ptot;
+      h = wht_stage<1>(h);
+      h = wht_stage<2>(h);
+      h = wht_stage<4>(h);
+      h = wht_stage<8>(h);
+      h = wht_stage<16>(h);
+      h = wht_stage<32>(h);
+      const int e = lane_pattern(lane);
+      if (e >= 0) s_red[wave][e] = h;
       if (energy) {
+        double vec[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vec[j] = zr[j];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           double z = 0.0;
 #pragma unroll
           for (int r = 0; r < kRegs; ++r) z += (((r >> j) ^ (r >> (j + 1))) & 1) ? -pr[r] : pr[r];
-          vec[5 + j] = z;
+          vec[4 + j] = z;
         }
-      }
-      const int e = lane_pattern(lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j >= 5 && !energy) break;
-        double h = vec[j];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const double o = __shfl_xor(h, 1 << k, 64);
-          h = ((lane >> k) & 1) ? o - h : h + o;
+        double zx = 0.0;
+        if (A.zx_reg >= 0) {
+          const double zj = A.zx_reg == 0 ? zr[0] : (A.zx_reg == 1 ? zr[1] : (A.zx_reg == 2 ? zr[2] : zr[3]));
+          zx = ((lane >> A.zx_lane) & 1) ? -zj : zj;
         }
-        if (e >= 0) s_red[wave][j * kRedLanes + e] = h;
+        vec[7] = zx;
+        const double r = wave_sum_multi<8>(vec);
+        if ((lane & 7) == 0) s_red[wave][kRedLanes + (lane >> 3)] = r;
+      } else {
+        const double r = wave_sum_multi<4>(zr);
+        if ((lane & 15) == 0) s_red[wave][kRedLanes + (lane >> 4)] = r;
       }
     }
     __syncthreads();
@@ -766,9 +864,12 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
             else waves |= 1 << (q - 6);
           }
         }
-        // registers: none -> total, one bit j -> z_j, adjacent bits j, j+1 -> zz_j
-        const int vi = regs == 0 ? 0 : (__popc(regs) == 1 ? 1 + __ffs(regs) - 1 : 5 + __ffs(regs) - 1);
-        const int slot = vi * kRedLanes + max(0, lane_pattern(lanes));
+        // registers: none -> the total's lane pattern; one bit j -> z_j (and
+        // with one lane bit: the host-chosen bond vector); adjacent bits j,
+        // j+1 -> zz_j
+        const int slot = regs == 0 ? max(0, lane_pattern(lanes))
+                         : (__popc(regs) == 1 ? (lanes ? kRedLanes + 7 : kRedLanes + __ffs(regs) - 1)
+                                              : kRedLanes + 4 + __ffs(regs) - 1);
         for (int w = 0; w < NW; ++w) acc += (__popc(w & waves) & 1) ? -s_red[w][slot] : s_red[w][slot];
         if (neg) acc = -acc;
       }
@@ -814,15 +915,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       }
       a[q] = x;
     }
-    const bool h5 = lane & 32, h4 = lane & 16;
-    double k0 = h5 ? a[2] : a[0], k1 = h5 ? a[3] : a[1];
-    const double s0 = h5 ? a[0] : a[2], s1 = h5 ? a[1] : a[3];
-    k0 += __shfl_xor(s0, 32, 64);
-    k1 += __shfl_xor(s1, 32, 64);
-    double k = h4 ? k1 : k0;
-    k += __shfl_xor(h4 ? k0 : k1, 16, 64);
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) k += __shfl_xor(k, off, 64);
+    const double k = wave_sum_multi<4>(a);
     if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = 2.0 * scale * k;
   };
   // squared share of the global factor carried by the factored kicks of
