@@ -427,9 +427,13 @@ def main(argv=None):
                         "GBps": launch_bytes / avg_lo / 1e9 if lo["launches"] else None},
             "kick_pass": {"launches": hi["launches"], "avg_ms": avg_hi * 1e3,
                         "GBps": launch_bytes / avg_hi / 1e9 if hi["launches"] else None},
+            "final_pass": {"launches": stats[4]["launches"], "avg_ms":
+                           stats[4]["total_ms"] / max(1, stats[4]["launches"]),
+                           "GBps": stats[4]["bytes"] / (stats[4]["total_ms"] / 1e3) / 1e9
+                           if stats[4]["launches"] else None,
+                           "note": "last pass of each echo chain: measure only, no store (16 B/amp)"},
             "reduce": {"launches": stats[2]["launches"], "total_ms": stats[2]["total_ms"]},
-            "kernel_time_frac": (lo["total_ms"] + hi["total_ms"] + stats[2]["total_ms"])
-            / (elapsed * 1e3),
+            "kernel_time_frac": sum(stats[k]["total_ms"] for k in stats) / (elapsed * 1e3),
         },
         "reference_equivalent": {
             "note": ("the reference runs one 1024-shot circuit per t (fwd and echo): "
@@ -715,7 +719,10 @@ def _pass_kernels(stats, elapsed):
             "kick_pass": {"launches": hi_s["launches"], "avg_ms": avg_hi * 1e3,
                           "GBps": hi_b / avg_hi / 1e9 if hi_s["launches"] else None},
             "reduce": {"launches": stats[2]["launches"], "total_ms": stats[2]["total_ms"]},
-            "kernel_time_frac": sum(stats[k]["total_ms"] for k in range(4)) / (elapsed * 1e3)}
+            "final_pass": {"launches": stats[4]["launches"], "total_ms": stats[4]["total_ms"],
+                           "GBps": stats[4]["bytes"] / (stats[4]["total_ms"] / 1e3) / 1e9
+                           if stats[4]["launches"] else None},
+            "kernel_time_frac": sum(stats[k]["total_ms"] for k in stats) / (elapsed * 1e3)}
     return roof, kern
 
 

@@ -273,7 +273,8 @@ int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_no
 #define DTC_KERNEL_HI_PASS 1   /* high-site kick pass                        */
 #define DTC_KERNEL_REDUCE 2    /* per-state observable reduction             */
 #define DTC_KERNEL_INIT 3      /* basis-state preparation                    */
-#define DTC_KERNEL_KINDS 4
+#define DTC_KERNEL_FINAL_PASS 4 /* last pass of an echo chain: measure, no store */
+#define DTC_KERNEL_KINDS 5
 int dtc_set_profiling(dtc_ctx* ctx, int32_t on);
 int dtc_kernel_stats(dtc_ctx* ctx, int32_t kind, int64_t* launches,
                      double* total_ms, double* total_bytes);

@@ -14,6 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
+KERNEL_KINDS = 5  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass
 ABI_VERSION = 6  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).

@@ -88,9 +88,9 @@ struct dtc_ctx {
   int prefix_n_traj = 0, prefix_device = 0;
   uint64_t prefix_hash = 0;
   bool prof = false;
-  int64_t st_n[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
-  double st_ms[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
-  double st_bytes[DTC_KERNEL_KINDS] = {0, 0, 0, 0};
+  int64_t st_n[DTC_KERNEL_KINDS] = {};
+  double st_ms[DTC_KERNEL_KINDS] = {};
+  double st_bytes[DTC_KERNEL_KINDS] = {};
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
   // sharded state (dtc_shard_*): device tables per bit map, cached so that
@@ -432,7 +432,8 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
 int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
                      int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
-                     const dtc::KickRec* recs = nullptr, int meas_parts = 0) {
+                     const dtc::KickRec* recs = nullptr, int meas_parts = 0,
+                     int no_store = 0) {
   const int shape = pass_shape(ps);
   if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
   const int kind = pass_kind(rc, ps, shape);
@@ -503,9 +504,11 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.meas = meas_mode;
   A.meas_at_end = meas_at_end;
   A.meas_parts = meas_parts;
+  A.no_store = no_store;
   A.batch = batch;
   A.n_obs = n_obs;
-  const int kernel = ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS;
+  const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
+                              : (ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->prof) {
     e0 = get_event(ctx);
@@ -515,8 +518,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream));
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
-    ctx->pending.push_back(
-        Pending{kernel, e0, e1, 32.0 * (double)((int64_t)1 << A.L_eff) * batch});
+    ctx->pending.push_back(Pending{kernel, e0, e1,
+                                   (no_store ? 16.0 : 32.0) * (double)((int64_t)1 << A.L_eff) * batch});
   }
   if (meas_mode != dtc::kMeasNone && meas_out)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
@@ -533,6 +536,7 @@ struct Launch {
   int meas_mode, meas_at_end, n_obs;
   double* meas_out;
   int64_t meas_stride;
+  int no_store = 0;  // the pass's output is never read again (last pass of an echo chain)
 };
 
 int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
@@ -556,7 +560,7 @@ int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
       const Launch& l = L[i0 + i];
       DTC_TRY(launch_pass_spec(ctx, rc, batch_start, batch, l.ps, l.src, l.dst, l.meas_mode,
                                l.meas_at_end, l.n_obs, l.meas_out, l.meas_stride,
-                               P.out + i * batch * dtc::kRecPerState));
+                               P.out + i * batch * dtc::kRecPerState, 0, l.no_store));
     }
   }
   return DTC_OK;
@@ -1101,6 +1105,9 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         }
         sched.back().meas_mode = dtc::kMeasProbe;
         sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;
+        // the echo state is only measured: the chain's last pass reads its
+        // tiles and stores nothing (the next chain starts from F again)
+        sched.back().no_store = 1;
       }
     }
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));

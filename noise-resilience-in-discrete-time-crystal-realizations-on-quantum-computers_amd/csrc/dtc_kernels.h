@@ -157,6 +157,7 @@ struct PassArgs {
   int meas_at_end;         // measure after the post-kick instead of after the diagonal
   int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 4 L_real
   int meas_parts;          // kMeasEnergy: MeasPart bits
+  int no_store;            // measure only: the tile is not written back (dst unused)
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]

@@ -601,7 +601,7 @@ struct RoundPlan {
 // MC, the measurements compiled in (separate instantiations, so a pass
 // carries only the code it can run): 0 = none, 1 = the probe, 2 = any mode
 // (per-site / energy Z), 3 = energy with the in-flight <X> points.
-template <int SHAPE, int NIBS, int KIND, int MC = 0>
+template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
@@ -1021,7 +1021,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   DTC_TS(5);
 
   char* dst = (char*)(A.dst + b * A.state_len);
-  if (ofs32) {
+  if constexpr (NS) {
+    // measurement-only pass (the last of an echo chain): nothing to write
+  } else if (ofs32) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
       char* a = dst + tile_ofs(r) + vofs;
@@ -1071,6 +1073,18 @@ DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
 DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
 #undef DTC_DEFINE_PASS
+// The last pass of an echo chain: same work, probe measurement, no stores
+// (the echo state is never read again): 16 B of HBM traffic per amplitude.
+#define DTC_DEFINE_FINAL(NAME, SHAPE_EXPR)                                         \
+  template <int NIBS, int KIND>                                                    \
+  __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
+    pass_body<SHAPE_EXPR, NIBS, KIND, 1, true>(A);                                 \
+  }
+DTC_DEFINE_FINAL(dtc_kdk_final, kShapeKDK)
+DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
+DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
+DTC_DEFINE_FINAL(dtc_kick_final, kShapeK)
+#undef DTC_DEFINE_FINAL
 template <int NIBS, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
   pass_body<kShapeD, NIBS, kKindRX, MC>(A);
@@ -1079,6 +1093,20 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
 template <int NIBS, int KIND, int MC>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
+  if (a.no_store) {
+    if constexpr (MC != 1) {
+      return hipErrorInvalidValue;  // only probe passes end an echo chain
+    } else {
+      switch (shape) {
+        case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        case kShapeKD: hipLaunchKernelGGL((dtc_kd_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        case kShapeDK: hipLaunchKernelGGL((dtc_dk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        case kShapeK: hipLaunchKernelGGL((dtc_kick_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
   switch (shape) {
     case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
     case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;

@@ -349,7 +349,7 @@ class DtcEngine:
 
     def kernel_stats(self):
         out = {}
-        for k in range(4):
+        for k in range(_capi.KERNEL_KINDS):
             n = ctypes.c_int64()
             ms = ctypes.c_double()
             by = ctypes.c_double()
