@@ -44,7 +44,9 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0    # float4 copy measured (same table)
-BOX_COPY_GBS = 5644.0        # best 16-B copy measured here (tools/tile_copy_bench.hip)
+BOX_COPY_GBS = 5715.0        # best read+write stream measured on this part (in place, 4 x 16 B
+                             # per lane; tools/hbm_ceiling.hip, profiles/r2d_hbm_ceiling.txt:
+                             # read alone 7.0-7.3 TB/s, write alone 5.2 TB/s)
 METRIC = "Floquet-periods×instances/sec at L=20; RZZ-kernel HBM GB/s vs peak"
 
 
