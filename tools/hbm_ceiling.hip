@@ -65,6 +65,39 @@ __global__ __launch_bounds__(256) void k_inplace(d2v* __restrict__ a, double c) 
   for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u] * c, &a[base + 256 * u]);
 }
 
+
+template <int U>
+__global__ __launch_bounds__(256) void k_write_plain(d2v* __restrict__ a) {
+  const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+  d2v z = {1.0, 2.0};
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[base + 256 * u] = z;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_inplace_plain(d2v* __restrict__ a, double c) {
+  const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+  d2v v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = a[base + 256 * u];
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[base + 256 * u] = v[u] * c;
+}
+
+// loads nontemporal, stores plain (and the reverse)
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_inplace_mix(d2v* __restrict__ a, double c) {
+  const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+  d2v v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = NTL ? __builtin_nontemporal_load(&a[base + 256 * u]) : a[base + 256 * u];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (NTS) __builtin_nontemporal_store(v[u] * c, &a[base + 256 * u]);
+    else a[base + 256 * u] = v[u] * c;
+  }
+}
+
 template <int LAYERS>
 __device__ __forceinline__ void fma_layers(d2v (&v)[16], double f) {
 #pragma unroll
@@ -192,6 +225,12 @@ int main() {
   rep("copy U=4", rw, time_it([&] { hipLaunchKernelGGL((k_copy<4>), dim3(n / 1024), dim3(256), 0, 0, a, b); }, 10));
   rep("copy U=16", rw, time_it([&] { hipLaunchKernelGGL((k_copy<16>), dim3(n / 4096), dim3(256), 0, 0, a, b); }, 10));
   rep("inplace U=4", rw, time_it([&] { hipLaunchKernelGGL((k_inplace<4>), dim3(n / 1024), dim3(256), 0, 0, a, 1.0); }, 10));
+  rep("write plain U=16", n * 16.0, time_it([&] { hipLaunchKernelGGL((k_write_plain<16>), dim3(n / 4096), dim3(256), 0, 0, b); }, 10));
+  rep("write plain U=4", n * 16.0, time_it([&] { hipLaunchKernelGGL((k_write_plain<4>), dim3(n / 1024), dim3(256), 0, 0, b); }, 10));
+  rep("inplace plain U=4", rw, time_it([&] { hipLaunchKernelGGL((k_inplace_plain<4>), dim3(n / 1024), dim3(256), 0, 0, a, 1.0); }, 10));
+  rep("inplace plain U=16", rw, time_it([&] { hipLaunchKernelGGL((k_inplace_plain<16>), dim3(n / 4096), dim3(256), 0, 0, a, 1.0); }, 10));
+  rep("inplace ntload/plainstore U=16", rw, time_it([&] { hipLaunchKernelGGL((k_inplace_mix<16, true, false>), dim3(n / 4096), dim3(256), 0, 0, a, 1.0); }, 10));
+  rep("inplace plainload/ntstore U=16", rw, time_it([&] { hipLaunchKernelGGL((k_inplace_mix<16, false, true>), dim3(n / 4096), dim3(256), 0, 0, a, 1.0); }, 10));
   rep("inplace U=16", rw, time_it([&] { hipLaunchKernelGGL((k_inplace<16>), dim3(n / 4096), dim3(256), 0, 0, a, 1.0); }, 10));
   const int tiles = (int)(n / 4096);
 #define RUN2(LY, EX)                                                                           \
