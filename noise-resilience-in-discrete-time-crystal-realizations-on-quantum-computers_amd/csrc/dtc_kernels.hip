@@ -508,7 +508,7 @@ __device__ __forceinline__ double wave_sum(double x) {
 template <int M>
 __device__ __forceinline__ double wht_stage(double h) {
   const double o = xor_lane<M>(h);
-  return (__lane_id() & M) ? o - h : h + o;
+  return fma((__lane_id() & M) ? -1.0 : 1.0, h, o);
 }
 
 // Sum of NV per-lane vectors over the wave (NV = 4 or 8), halving the vector
@@ -749,25 +749,30 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // tile's stores are issued (probe_finish), off the pass's critical path
   double pm_tot = 0.0, pm_z = 0.0, pm_inv = 1.0;
   bool pm_on = false;
+  int zc_lay = -1;  // MC >= 2: layout of a measurement whose combine is pending
+  double zc_inv = 1.0;
   auto measure_in = [&](auto lay_tag, double inv_w2) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
     const int wave = t >> 6, lane = t & 63;
-    double pr[kRegs];
-    double ptot = 0.0;
+    // w[m] = sum_r (-1)^popcount(r & m) |a_r|^2: the total (m = 0), z of each
+    // register bit (m = 1 << j) and z z of adjacent register bits (m = 3 << j)
+    // by one in-register 16-point Walsh-Hadamard transform (64 adds)
+    double w[kRegs];
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      pr[r] = v[r].x * v[r].x + v[r].y * v[r].y;
-      ptot += pr[r];
+    for (int r = 0; r < kRegs; ++r) w[r] = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        if (r & (1 << b)) continue;
+        const double lo = w[r], hi = w[r | (1 << b)];
+        w[r] = lo + hi;
+        w[r | (1 << b)] = lo - hi;
+      }
     }
-    double zr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double z = 0.0;
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) z += ((r >> j) & 1) ? -pr[r] : pr[r];
-      zr[j] = z;
-    }
+    const double ptot = w[0];
+    const double zr[4] = {w[1], w[2], w[4], w[8]};
     const bool probe_only = MC <= 1 || A.meas == kMeasProbe;
     const bool energy = MC >= 2 && A.meas == kMeasEnergy;
     auto tile_bit = [&](int site) {
@@ -816,13 +821,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         double vec[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) vec[j] = zr[j];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          double z = 0.0;
-#pragma unroll
-          for (int r = 0; r < kRegs; ++r) z += (((r >> j) ^ (r >> (j + 1))) & 1) ? -pr[r] : pr[r];
-          vec[4 + j] = z;
-        }
+        vec[4] = w[3];
+        vec[5] = w[6];
+        vec[6] = w[12];
         double zx = 0.0;
         if (A.zx_reg >= 0) {
           const double zj = A.zx_reg == 0 ? zr[0] : (A.zx_reg == 1 ? zr[1] : (A.zx_reg == 2 ? zr[2] : zr[3]));
@@ -836,46 +837,59 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         if ((lane & 15) == 0) s_red[wave][kRedLanes + (lane >> 4)] = r;
       }
     }
-    __syncthreads();
-    const int n_mid = probe_only ? 2 : (energy ? 2 * A.L_real : 1 + A.L_real);
-    if (t < n_mid) {
-      constexpr int NW = kThreads / 64;
-      double acc = 0.0;
-      if (probe_only) {
+    if (probe_only) {
+      __syncthreads();
+      if (t < 2) {
+        double acc = 0.0;
         const int site = A.probe;
         const int ws = (t == 0 || tile_bit(site) >= 0) ? t : 0;
-        for (int w = 0; w < NW; ++w) acc += s_red[w][ws];
+        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][ws];
         if (ws != t && ((M.tbase >> site) & 1)) acc = -acc;
-      } else if constexpr (MC >= 2) {
-        // observable t: 0 norm, 1..L Z_{t-1}, L+1.. Z_i Z_i+1 (i = t-1-L)
-        const int i0 = t <= A.L_real ? t - 1 : t - 1 - A.L_real;
-        const int ns = t == 0 ? 0 : (t <= A.L_real ? 1 : 2);
-        int regs = 0, lanes = 0, waves = 0, neg = 0;
-        for (int k = 0; k < ns; ++k) {
-          const int site = i0 + k;
-          const int tb = tile_bit(site);
-          if (tb < 0) {
-            neg ^= (int)((M.tbase >> site) & 1);
-          } else if (tb >= 4 * LAY && tb < 4 * LAY + 4) {
-            regs |= 1 << (tb - 4 * LAY);
-          } else {
-            const int q = LAY == 2 ? tb : (LAY == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
-            if (q < 6) lanes |= 1 << q;
-            else waves |= 1 << (q - 6);
-          }
-        }
-        // registers: none -> the total's lane pattern; one bit j -> z_j (and
-        // with one lane bit: the host-chosen bond vector); adjacent bits j,
-        // j+1 -> zz_j
-        const int slot = regs == 0 ? max(0, lane_pattern(lanes))
-                         : (__popc(regs) == 1 ? (lanes ? kRedLanes + 7 : kRedLanes + __ffs(regs) - 1)
-                                              : kRedLanes + 4 + __ffs(regs) - 1);
-        for (int w = 0; w < NW; ++w) acc += (__popc(w & waves) & 1) ? -s_red[w][slot] : s_red[w][slot];
-        if (neg) acc = -acc;
+        A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc * inv_w2;
       }
-      acc *= inv_w2;
-      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    } else {
+      // combined after the tile's stores are issued (meas_finish)
+      zc_lay = LAY;
+      zc_inv = inv_w2;
     }
+  };
+  // Per-site / energy Z, ZZ partials of the tile from the wave sums in s_red
+  // (layout lay of the measurement): one observable per thread t < n_mid.
+  auto site_combine = [&](int lay, double inv_w2) {
+    const bool energy = MC >= 2 && A.meas == kMeasEnergy;
+    const int n_mid = energy ? 2 * A.L_real : 1 + A.L_real;
+    if (t >= n_mid) return;
+    auto tile_bit = [&](int site) {
+      return site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+    };
+    constexpr int NW = kThreads / 64;
+    double acc = 0.0;
+    // observable t: 0 norm, 1..L Z_{t-1}, L+1.. Z_i Z_i+1 (i = t-1-L)
+    const int i0 = t <= A.L_real ? t - 1 : t - 1 - A.L_real;
+    const int ns = t == 0 ? 0 : (t <= A.L_real ? 1 : 2);
+    int regs = 0, lanes = 0, waves = 0, neg = 0;
+    for (int k = 0; k < ns; ++k) {
+      const int site = i0 + k;
+      const int tb = tile_bit(site);
+      if (tb < 0) {
+        neg ^= (int)((M.tbase >> site) & 1);
+      } else if (tb >= 4 * lay && tb < 4 * lay + 4) {
+        regs |= 1 << (tb - 4 * lay);
+      } else {
+        const int q = lay == 2 ? tb : (lay == 1 ? (tb < 4 ? tb : tb - 4) : tb - 4);
+        if (q < 6) lanes |= 1 << q;
+        else waves |= 1 << (q - 6);
+      }
+    }
+    // registers: none -> the total's lane pattern; one bit j -> z_j (and
+    // with one lane bit: the host-chosen bond vector); adjacent bits j,
+    // j+1 -> zz_j
+    const int slot = regs == 0 ? max(0, lane_pattern(lanes))
+                     : (__popc(regs) == 1 ? (lanes ? kRedLanes + 7 : kRedLanes + __ffs(regs) - 1)
+                                          : kRedLanes + 4 + __ffs(regs) - 1);
+    for (int w = 0; w < NW; ++w) acc += (__popc(w & waves) & 1) ? -s_red[w][slot] : s_red[w][slot];
+    if (neg) acc = -acc;
+    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc * inv_w2;
   };
   auto probe_finish = [&]() {
     const int wave = t >> 6, lane = t & 63;
@@ -1001,23 +1015,6 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (MC > 0) {
     if (A.meas != kMeasNone && A.meas_at_end) measure_in(LIO{}, 1.0);
   }
-  if (x_pre || x_post) {
-    // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
-    // (0 for sites this pass does not kick)
-    __syncthreads();
-    const int L = A.L_real;
-    if (t >= 2 * L && t < 4 * L) {
-      const bool pre = t >= 3 * L;
-      const int site = pre ? t - 3 * L : t - 2 * L;
-      const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
-      double acc = 0.0;
-      if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
-        const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
-        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
-      }
-      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
-    }
-  }
   DTC_TS(5);
 
   char* dst = (char*)(A.dst + b * A.state_len);
@@ -1048,6 +1045,30 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   if constexpr (MC == 1) {
     if (pm_on) probe_finish();  // workgroup-uniform (A.meas)
+  }
+  if constexpr (MC >= 2) {
+    // measurement combines after the tile's stores are issued (one barrier)
+    if (zc_lay >= 0 || x_pre || x_post) {
+      __syncthreads();
+      if (zc_lay >= 0) site_combine(zc_lay, zc_inv);
+      if (x_pre || x_post) {
+        // (after the stores: meas_finish)
+        // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
+        // (0 for sites this pass does not kick)
+        const int L = A.L_real;
+        if (t >= 2 * L && t < 4 * L) {
+          const bool pre = t >= 3 * L;
+          const int site = pre ? t - 3 * L : t - 2 * L;
+          const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+          double acc = 0.0;
+          if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
+            const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
+            for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
+          }
+          A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+        }
+      }
+    }
   }
 #ifdef DTC_PHASE_TIMING
   DTC_TS(6);
