@@ -192,6 +192,23 @@ def spawn_selftest(args) -> int:
     return 0
 
 
+def _device_and_backend(local_rank, world):
+    """GPU of this rank and the process-group backend.  Normal runs: GPU
+    local_rank, RCCL ("nccl").  BENCH_SHARE_DEVICE=1 (plumbing test on a 1-GPU
+    box, tests/test_gpu_bench_spawn.py): every rank on GPU 0 with the backend
+    BENCH_DIST_BACKEND (gloo: RCCL refuses two ranks on one GPU); the numbers
+    of such a run say nothing about scaling."""
+    share = os.environ.get("BENCH_SHARE_DEVICE") == "1"
+    dev = 0 if (share or world == 1) else local_rank
+    backend = os.environ.get("BENCH_DIST_BACKEND", "gloo" if share else "nccl")
+    return dev, backend
+
+
+def _coll_dev(backend):
+    """Where the (few-KB) collective buffers live: the GPU for RCCL, host for gloo."""
+    return "cuda" if backend == "nccl" else "cpu"
+
+
 def host_cpu_info() -> dict:
     """CPU model and the cores this process may use: the affinity set, capped
     by a cgroup CPU quota when one is set (a GPU box's share of its host)."""
@@ -283,13 +300,13 @@ def main(argv=None):
     import torch
 
     dist = None
+    dev, backend = _device_and_backend(local_rank, world)
+    cdev = _coll_dev(backend)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group(backend)
 
     pkg = importlib.import_module(PKG)
     hs, phis = load_disorder_row(args.L)
@@ -302,7 +319,7 @@ def main(argv=None):
         spec.device = cal.device_noise(args.L)
         if args.batch == 256:
             args.batch = 1024
-    eng = pkg.DtcEngine(local_rank)
+    eng = pkg.DtcEngine(dev)
     B = args.batch
     if args.strong_total:
         # SURVEY.md §8(d) scaling report (north_star: >= 6x strong scaling 1 -> 8
@@ -332,7 +349,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    acc = torch.from_numpy(sums).cuda()
+    acc = torch.from_numpy(sums).to(cdev)
     if dist:
         dist.all_reduce(acc)  # RCCL over xGMI: the only collective (final autocorr gather)
     torch.cuda.synchronize()
@@ -342,14 +359,14 @@ def main(argv=None):
     eng.set_profiling(False)
     stats = eng.kernel_stats()
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     autocorr = (acc.cpu().numpy() / (world * args.steps * B))
     # every rank's K-D-K pass rate (the north_star's per-GPU roofline at N GPUs)
     my = torch.tensor([stats[0]["total_ms"], float(stats[0]["launches"]), elapsed],
-                      dtype=torch.float64, device="cuda")
+                      dtype=torch.float64, device=cdev)
     per_rank = [my]
     if dist:
         per_rank = [torch.zeros_like(my) for _ in range(world)]
@@ -466,14 +483,16 @@ def main_c4(args):
     import torch
 
     dist = None
-    torch.cuda.set_device(local_rank if world > 1 else 0)
+    dev, backend = _device_and_backend(local_rank, world)
+    cdev = _coll_dev(backend)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     pkg = importlib.import_module(PKG)
     L, T, n = 28, args.tf, args.instances
-    eng = pkg.DtcEngine(local_rank)
+    eng = pkg.DtcEngine(dev)
     sums = np.zeros((T, L))
 
     def step(i):
@@ -494,7 +513,7 @@ def main_c4(args):
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    acc = torch.from_numpy(sums).cuda()
+    acc = torch.from_numpy(sums).to(cdev)
     if dist:
         dist.all_reduce(acc)  # the only collective: per-site <Z_i(t)> sums
     torch.cuda.synchronize()
@@ -503,7 +522,7 @@ def main_c4(args):
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
     stats = eng.kernel_stats()
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -656,19 +675,26 @@ def main_c5(args):
         dist.destroy_process_group()
 
 
+_CDEV = "cuda"
+
+
 def _init_dist():
+    """(world, rank, device ordinal, torch.distributed or None) of this rank."""
+    global _CDEV
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
     dist = None
-    torch.cuda.set_device(local_rank if world > 1 else 0)
+    dev, backend = _device_and_backend(local_rank, world)
+    _CDEV = _coll_dev(backend)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
-    return world, rank, local_rank, dist
+        dist.init_process_group(backend)
+    return world, rank, dev, dist
 
 
 def _timed(eng, dist, warmup, steps, step, reduce_buf):
@@ -688,7 +714,7 @@ def _timed(eng, dist, warmup, steps, step, reduce_buf):
     t0 = time.perf_counter()
     for i in range(steps):
         step(warmup + i)
-    acc = torch.from_numpy(reduce_buf).cuda()
+    acc = torch.from_numpy(reduce_buf).to(_CDEV)
     if dist:
         dist.all_reduce(acc)
     torch.cuda.synchronize()
@@ -697,7 +723,7 @@ def _timed(eng, dist, warmup, steps, step, reduce_buf):
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
     stats = eng.kernel_stats()
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=_CDEV)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return float(el.item()), acc.cpu().numpy(), stats
