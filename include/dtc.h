@@ -204,22 +204,26 @@ int dtc_shard_step_async(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise*
                          int32_t period, uint64_t pre_mask, int32_t diag, uint64_t post_mask,
                          const double* src, double* dst, double* obs_dev);
 
-/* The period-`period` kick on the local bits pre_mask, restricted to chunk
- * `chunk` of every shard held: the amplitudes whose top chunk_bits local bits
- * equal `chunk` (in place; asynchronous, ctx stream).  pre_mask must lie below
- * the chunk bits.  With chunk_bits = n_global this is the part of a period's
- * pre-exchange kicks that feeds one destination rank, so the sweep driver can
- * send chunk c while chunk c+1 is kicked (sharded.py). */
-int dtc_shard_kick_chunk(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+/* The period-`period` kick on the local bits pre_mask, restricted to slice
+ * `slice` of every chunk of every shard held: a shard's top chunk_bits local
+ * bits number its chunks, the next slice_bits its slices, so the call covers the
+ * amplitudes whose slice bits equal `slice` (in place; asynchronous, ctx stream;
+ * one launch).  pre_mask must lie below the slice bits.  With chunk_bits =
+ * n_global, chunk c is what rank c receives in the period's all-to-all; the
+ * sweep driver kicks slice s+1 while slice s of every chunk travels to every
+ * peer at once (sharded.py). */
+int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
                          const dtc_shard* shard, uint64_t seed, int64_t traj, int32_t period,
-                         uint64_t pre_mask, int32_t chunk_bits, int32_t chunk, double* state);
+                         uint64_t pre_mask, int32_t chunk_bits, int32_t slice_bits,
+                         int32_t slice, double* state);
 
 /* The ctx's HIP stream (hipStream_t), for ordering host-side collectives
  * against the asynchronous entry points; and a wait for everything on it. */
 int dtc_get_stream(dtc_ctx* ctx, void** stream);
 int dtc_synchronize(dtc_ctx* ctx);
 
-/* Host-only: the site groups the engine's passes use for an n_bits-bit state
+/* Host-only: the site groups the engine's sharded steps use for an n_bits-bit
+ * shard (high groups in increasing size: the top bits lie in a large group)
  * (bit masks, one per group; returns the count or a negative error). */
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups);
 

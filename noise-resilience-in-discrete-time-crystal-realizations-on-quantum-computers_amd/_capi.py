@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "dtc_autocorr_prefixed",
     "dtc_prefix_release",
     "dtc_shard_step_async",
-    "dtc_shard_kick_chunk",
+    "dtc_shard_kick_slice",
     "dtc_get_stream",
     "dtc_synchronize",
 )
@@ -188,10 +188,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ]
-        lib.dtc_shard_kick_chunk.argtypes = [
+        lib.dtc_shard_kick_slice.argtypes = [
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
-            ctypes.c_void_p,
+            ctypes.c_int32, ctypes.c_void_p,
         ]
         lib.dtc_get_stream.argtypes = [ctypes.c_void_p, P(ctypes.c_void_p)]
         lib.dtc_synchronize.argtypes = [ctypes.c_void_p]

@@ -167,7 +167,11 @@ struct Plan {
 // diag_in: one window-table lookup per amplitude): the low group holds 9..12
 // sites, a higher group 9, 8 or 4 (c = 3, 4, 8).  Fewest groups first, then
 // the largest low group, then the largest higher groups.
-Plan make_plan(int L) {
+// largest_top (sharded states): the high groups in increasing size, so the
+// group holding the top bits (the bits an exchange swaps with the rank bits)
+// is a large one and the pre-exchange kicks stay below a few free bits of it
+// (the slices of dtc_shard_kick_slice).
+Plan make_plan(int L, bool largest_top = false) {
   Plan pl;
   pl.L = L;
   pl.L_eff = std::max(L, dtc::kTileBits);
@@ -192,7 +196,8 @@ Plan make_plan(int L) {
           if (9 * n9 + 8 * n8 + 4 * n4 != need) continue;
           pl.groups.push_back(Group{0, 0, (1 << a_lo) - 1});
           int s = a_lo;
-          for (int k = 0; k < 3; ++k) {
+          for (int kk = 0; kk < 3; ++kk) {
+            const int k = largest_top ? 2 - kk : kk;
             const int cnt = k == 0 ? n9 : (k == 1 ? n8 : n4);
             for (int i = 0; i < cnt; ++i) {
               const int a = kHi[k], c = dtc::kTileBits - a;
@@ -449,6 +454,10 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   }
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
   const Group& g = rc.pl.groups[ps.group];
+#ifdef DTC_PHASE_TIMING
+  if (const char* e = std::getenv("DTC_DBG_GROUP"))
+    if (std::atoi(e) != ps.group) A.dbg_ts = nullptr;
+#endif
   A.zx_reg = -1;
   A.zx_lane = -1;
   if (meas_mode == dtc::kMeasEnergy) {
@@ -1520,7 +1529,7 @@ int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_nois
 
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups) {
   if (n_bits < 1 || n_bits > 40 || !masks) return fail(DTC_EINVAL, "bad arguments");
-  Plan pl = make_plan(n_bits);
+  Plan pl = make_plan(n_bits, true);
   if ((int)pl.groups.size() > max_groups) return fail(DTC_EINVAL, "max_groups too small");
   for (size_t g = 0; g < pl.groups.size(); ++g)
     masks[g] = group_bits(pl.groups[g]) & ((n_bits >= 64) ? ~0ull : ((1ull << n_bits) - 1));
@@ -1641,7 +1650,7 @@ RunCfg shard_runcfg(const dtc_problem* pr, const dtc_noise* nz, const dtc_shard*
                     uint64_t seed, int64_t traj) {
   RunCfg rc;
   rc.prob = pr;
-  rc.pl = make_plan(sh->n_local);
+  rc.pl = make_plan(sh->n_local, true);
   rc.seed = seed;
   rc.traj_offset = traj;
   rc.n_traj = 1;  // batch index b = shard b -> diag table b
@@ -1762,37 +1771,44 @@ int dtc_shard_step_async(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* n
                          src, dst, obs_dev, true);
 }
 
-int dtc_shard_kick_chunk(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                          const dtc_shard* sh, uint64_t seed, int64_t traj, int32_t period,
-                         uint64_t pre_mask, int32_t chunk_bits, int32_t chunk, double* state) {
+                         uint64_t pre_mask, int32_t chunk_bits, int32_t slice_bits, int32_t slice,
+                         double* state) {
   if (!state) return fail(DTC_EINVAL, "null state");
   DTC_TRY(shard_check_common(ctx, pr, nz, sh, traj, 0));
   const int nl = sh->n_local;
-  if (chunk_bits < 0 || chunk_bits > 16 || nl - chunk_bits < dtc::kTileBits)
-    return fail(DTC_EINVAL, "chunk_bits must leave >= 12 bits per chunk");
-  if (chunk < 0 || chunk >= (1 << chunk_bits)) return fail(DTC_EINVAL, "chunk out of range");
-  const int nsub = nl - chunk_bits;
+  if (chunk_bits < 0 || slice_bits < 0 || chunk_bits + slice_bits > 16 ||
+      nl - chunk_bits - slice_bits < dtc::kTileBits)
+    return fail(DTC_EINVAL, "chunk_bits + slice_bits must leave >= 12 bits per slice");
+  if (slice < 0 || slice >= (1 << slice_bits)) return fail(DTC_EINVAL, "slice out of range");
+  const int nsub = nl - chunk_bits - slice_bits;
   const uint64_t low = (1ull << nsub) - 1;
-  if (pre_mask & ~low) return fail(DTC_EINVAL, "chunk kick mask reaches the chunk bits");
+  if (pre_mask & ~low) return fail(DTC_EINVAL, "slice kick mask reaches the chunk/slice bits");
   const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
   if (!pre_mask) return DTC_OK;
   if (period < 1 || period > n_rows) return fail(DTC_EINVAL, "period outside kick table");
+  const int64_t n_pieces = (int64_t)sh->n_shards << chunk_bits;
+  if (n_pieces > 65535) return fail(DTC_EINVAL, "too many chunks x shards for one launch");
   DTC_HIP(hipSetDevice(ctx->device));
   RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
   const Plan& pl = rc.pl;
   DTC_TRY(shard_tables(ctx, pr, sh, 0, pl, rc));
+  // one launch: the slice of every (shard, chunk) piece is a 2^nsub-amplitude
+  // state, pieces 2^(nl - chunk_bits) apart (the same trajectory: identical
+  // kick records for every piece)
   rc.L_eff_override = nsub;
-  rc.stride_override = (int64_t)1 << nl;
-  double2* base = (double2*)state + ((size_t)chunk << nsub);
+  rc.stride_override = (int64_t)1 << (nl - chunk_bits);
+  double2* base = (double2*)state + ((size_t)slice << nsub);
   for (size_t g = 0; g < pl.groups.size(); ++g) {
     const Group& G = pl.groups[g];
     const uint64_t gb = group_bits(G);
     if (!(pre_mask & gb)) continue;
-    if (gb & ~low) return fail(DTC_EINVAL, "a site group of the kick mask reaches the chunk bits");
+    if (gb & ~low) return fail(DTC_EINVAL, "a site group of the kick mask reaches the slice bits");
     PassSpec ps{(int)g, no_kick(), no_kick(), dtc::kDiagNone, 0};
     ps.pre = dtc::KickDesc{1, period - 1, dtc::kKickForward, dtc::kStreamForward,
                            (uint32_t)period, skip_bits(G, pre_mask)};
-    DTC_TRY(launch_pass_spec(ctx, rc, 0, sh->n_shards, ps, base, base, dtc::kMeasNone, 1, 2,
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, (int)n_pieces, ps, base, base, dtc::kMeasNone, 1, 2,
                              nullptr, 0));
   }
   return DTC_OK;

@@ -511,29 +511,52 @@ __device__ __forceinline__ double wht_stage(double h) {
   return fma((__lane_id() & M) ? -1.0 : 1.0, h, o);
 }
 
+// permlane{32,16}_swap of a pair of doubles (both 32-bit halves): with
+// vdst = a, src0 = b, a becomes (a's lower half-wave / even rows, b's lower /
+// even) and b becomes (a's upper / odd, b's upper / odd).  For a pair whose
+// first member is kept by the lanes without the bit and the second by the
+// lanes with it, a + b afterwards is, in every lane, its kept vector summed
+// with the partner lane's copy: one swap pair and one add per stage, no
+// selects, no copies.
+template <int M>
+__device__ __forceinline__ void swap_rows(double& a, double& b) {
+  const long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
+  const int alo = (int)(ab & 0xffffffffll), ahi = (int)(ab >> 32);
+  const int blo = (int)(bb & 0xffffffffll), bhi = (int)(bb >> 32);
+  if constexpr (M == 32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
+    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
+  } else {
+    static_assert(M == 16, "row swap");
+    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
+    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
+  }
+}
+
 // Sum of NV per-lane vectors over the wave (NV = 4 or 8), halving the vector
 // count per lane at each of the first stages: afterwards every lane of the
 // group of 8 with lane bits (5, 4, 3) = v (NV = 8; NV = 4: bits (5, 4)
-// and every bit-3 value) holds the wave sum of vector v.  NV/2 + NV/4 + ...
-// lane exchanges instead of 6 NV.
+// and every bit-3 value) holds the wave sum of vector v.
 template <int NV>
 __device__ __forceinline__ double wave_sum_multi(const double (&x)[NV]) {
   const int lane = __lane_id();
   double a[NV / 2];
-  const bool h5 = lane & 32;
 #pragma unroll
   for (int m = 0; m < NV / 2; ++m) {
-    const double keep = h5 ? x[NV / 2 + m] : x[m];
-    const double send = h5 ? x[m] : x[NV / 2 + m];
-    a[m] = keep + xor_lane<32>(send);
+    double u = x[m], w = x[NV / 2 + m];
+    swap_rows<32>(u, w);
+    a[m] = u + w;
   }
-  const bool h4 = lane & 16;
   double b[NV / 4];
 #pragma unroll
   for (int m = 0; m < NV / 4; ++m) {
-    const double keep = h4 ? a[NV / 4 + m] : a[m];
-    const double send = h4 ? a[m] : a[NV / 4 + m];
-    b[m] = keep + xor_lane<16>(send);
+    double u = a[m], w = a[NV / 4 + m];
+    swap_rows<16>(u, w);
+    b[m] = u + w;
   }
   double c;
   if constexpr (NV == 8) {

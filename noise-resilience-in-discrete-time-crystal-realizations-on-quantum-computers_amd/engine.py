@@ -320,16 +320,17 @@ class DtcEngine:
             ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr),
             ctypes.c_void_p(obs_ptr) if obs_ptr else None))
 
-    def shard_kick_chunk(self, spec: SweepSpec, shard, period: int, pre_mask: int,
-                         chunk_bits: int, chunk: int, state_ptr: int, seed: int = 0x5EED0001,
-                         traj: int = 0):
-        """K_period on the local bits pre_mask of chunk `chunk` (top chunk_bits
-        local bits) of every shard held, in place, asynchronously."""
-        _capi.check(self._lib.dtc_shard_kick_chunk(
+    def shard_kick_slice(self, spec: SweepSpec, shard, period: int, pre_mask: int,
+                         chunk_bits: int, slice_bits: int, slice_: int, state_ptr: int,
+                         seed: int = 0x5EED0001, traj: int = 0):
+        """K_period on the local bits pre_mask of slice `slice_` of every chunk
+        (top chunk_bits local bits; the next slice_bits number the slices) of
+        every shard held, in place, asynchronously (one launch)."""
+        _capi.check(self._lib.dtc_shard_kick_slice(
             self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
             ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
             ctypes.c_int32(period), ctypes.c_uint64(pre_mask), ctypes.c_int32(chunk_bits),
-            ctypes.c_int32(chunk), ctypes.c_void_p(state_ptr)))
+            ctypes.c_int32(slice_bits), ctypes.c_int32(slice_), ctypes.c_void_p(state_ptr)))
 
     def stream_handle(self) -> int:
         """The engine's hipStream_t (for torch.cuda.ExternalStream)."""

@@ -159,9 +159,10 @@ class EngineStepper:
             self._stream = torch.cuda.ExternalStream(self.engine.stream_handle())
         return self._stream
 
-    def kick_chunk(self, spec, layout, seed, traj, period, pre, chunk_bits, chunk, buf):
-        self.engine.shard_kick_chunk(spec, layout.to_c(), period, pre, chunk_bits, chunk,
-                                     buf.data_ptr(), seed, traj)
+    def kick_slice(self, spec, layout, seed, traj, period, pre, chunk_bits, slice_bits, slice_,
+                   buf):
+        self.engine.shard_kick_slice(spec, layout.to_c(), period, pre, chunk_bits, slice_bits,
+                                     slice_, buf.data_ptr(), seed, traj)
 
     def step_async(self, spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
                    obs_out):
@@ -266,46 +267,42 @@ def sharded_forward(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0, t
 
 # ---- the pipelined sweep (C5 on the GPU node) -----------------------------------------
 
-class _ChunkExchange:
-    """All-to-all of one period as W chunk transfers, each started as soon as
-    its chunk has been kicked.
+class _SliceExchange:
+    """All-to-all of one period as S slice transfers, each started as soon as
+    its slice has been kicked.
 
-    Collective (one shard per process): at step i rank r sends its chunk
-    (r + i) mod W to that rank and receives chunk r of rank (r - i) mod W into
-    position (r - i) mod W (step 0: a local copy) -- every rank runs step i at
-    the same time, so the point-to-point pairs always match.  The transfers run
-    on a side stream that waits for the kick of their chunk (an event on the
-    engine stream); the engine stream waits for all of them before the fused
-    pass.  Virtual ranks (one process): chunk c of every shard is copied to
-    shard c on the side stream.  CPU tensors (gloo tests): the same transfers,
+    A shard's top n_global local bits number its chunks (chunk c goes to rank
+    c), the next slice_bits number the slices of every chunk.  Step s sends
+    slice s of every chunk to its rank and receives slice s of this rank's
+    chunk from every rank -- all peers at once, so every xGMI link carries a
+    transfer (one ``batch_isend_irecv`` of 7 sends and 7 receives at 8 ranks;
+    the local slice is a device copy).  The transfers run on a side stream
+    that waits for the slice's kick (an event on the engine stream); the
+    engine stream waits for all of them before the fused pass.  Virtual ranks
+    (one process): slice s of every chunk of every shard is copied to its shard
+    on the side stream.  CPU tensors (gloo tests): the same transfers,
     synchronously."""
 
-    def __init__(self, stepper, W, rank, world, group):
+    def __init__(self, stepper, W, S, rank, world, group):
         import torch
 
-        self.W, self.rank, self.world, self.group = W, rank, world, group
+        self.W, self.S, self.rank, self.world, self.group = W, S, rank, world, group
         self.cuda = hasattr(stepper, "stream")
         self.eng = stepper.stream() if self.cuda else None
         self.side = torch.cuda.Stream() if self.cuda else None
         self.works = []
         self.t_events = []  # (start, end) per period, side stream
 
-    def order(self):
-        """Chunk kicked at step i: the destination rank of that step."""
-        if self.world == 1:
-            return list(range(self.W))
-        return [(self.rank + i) % self.W for i in range(self.W)]
-
-    def send(self, i, chunk, src, dst):
+    def send(self, s, src, dst):
         import torch
         import torch.distributed as dist
 
-        W = self.W
+        W, S = self.W, self.S
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(self.eng)
             self.side.wait_event(ev)
-            if i == 0:
+            if s == 0:
                 start = torch.cuda.Event(enable_timing=True)
                 start.record(self.side)
                 self.t_events.append([start, None])
@@ -316,21 +313,22 @@ class _ChunkExchange:
             ctx = contextlib.nullcontext()
         with ctx:
             if self.world == 1:
-                dst.view(W, W, -1)[chunk].copy_(src.view(W, W, -1)[:, chunk])
+                dst.view(W, W, S, -1)[:, :, s].copy_(src.view(W, W, S, -1)[:, :, s].transpose(0, 1))
                 return
-            s_rank = (self.rank - i) % W
-            sv, dv = src.view(W, -1), dst.view(W, -1)
-            if i == 0:
-                dv[self.rank].copy_(sv[self.rank])
-                return
-            ops = [dist.P2POp(dist.isend, torch.view_as_real(sv[chunk]), chunk, self.group),
-                   dist.P2POp(dist.irecv, torch.view_as_real(dv[s_rank]), s_rank, self.group)]
+            sv, dv = src.view(W, S, -1), dst.view(W, S, -1)
+            r = self.rank
+            dv[r, s].copy_(sv[r, s])
+            ops = []
+            for i in range(1, W):
+                d, q = (r + i) % W, (r - i) % W
+                ops.append(dist.P2POp(dist.isend, torch.view_as_real(sv[d, s]), d, self.group))
+                ops.append(dist.P2POp(dist.irecv, torch.view_as_real(dv[q, s]), q, self.group))
             reqs = dist.batch_isend_irecv(ops)
             if self.cuda:
                 self.works.extend(reqs)
             else:
-                for r in reqs:
-                    r.wait()
+                for q in reqs:
+                    q.wait()
 
     def finish(self):
         import torch
@@ -360,11 +358,11 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
 
     Per period: the pre-exchange kicks (every local site group except the one
     holding the top bits, which the previous fused pass already kicked) run
-    chunk by chunk -- chunk c = the amplitudes with top n_global local bits c
-    = what rank c receives -- and each chunk's transfer starts as soon as it is
-    kicked, while the next chunk is kicked; then the fused pass (kick of the
-    newly local sites, RZZ/RZ, measurement, next kick of the top group) runs
-    on the received shard.  The first period also kicks the top group itself
+    slice by slice -- chunk c (top n_global local bits = c) is what rank c
+    receives, and slice s of every chunk is kicked in one launch -- and slice
+    s travels to every peer at once while slice s+1 is kicked; then the fused
+    pass (kick of the newly local sites, RZZ/RZ, measurement, next kick of the
+    top group) runs on the received shard.  The first period also kicks the top group itself
     (one whole-shard pass) before its chunks.  Observables go to a device
     array; the host reads them once at the end and joins the ranks with one
     all-reduce.  Same results as ``sharded_forward``.
@@ -386,11 +384,18 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     if any(g & top for g in groups if g != main):
         raise ValueError("the top local bits must all lie in one site group")
     post_bits = main | top
-    chunked = nl - n_global >= 12  # a chunk holds at least one 4096-amplitude tile
+    # slices: the free bits of the top group just below the rank-swapped bits
+    # (above every bit the pre-exchange kicks touch), at most 8 slices, each at
+    # least one 4096-amplitude tile per chunk
+    tile = getattr(stepper, "min_slice_index_bits", 12)
+    pre_top = max((g.bit_length() - 1 for g in groups if g != main), default=-1)
+    slice_bits = max(0, min(3, nl - n_global - 1 - pre_top, nl - n_global - tile))
+    chunked = nl - n_global - slice_bits >= tile
+    S = 1 << slice_bits if chunked else 1
     P = T - 1 + spec.t_offset
     obs = stepper.obs_buffer(P + 1, n_sh, 1 + nl)
     layouts = [lay]
-    xch = _ChunkExchange(stepper, W, rank, world, group)
+    xch = _SliceExchange(stepper, W, S, rank, world, group)
 
     stepper.set_basis(spec, lay, seed, traj, A)
     stepper.step_async(spec, lay, seed, traj, inst, 1, 0, False, 0, A, A, obs[0])
@@ -403,10 +408,11 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
             whole = pre if not chunked else pre & post_bits
             stepper.step_async(spec, lay, seed, traj, inst, p, whole, False, 0, A, A, None)
             pre &= ~whole
-        for i, c in enumerate(xch.order()):
+        for sl in range(S):
             if pre:
-                stepper.kick_chunk(spec, lay, seed, traj, p, pre, n_global, c, A)
-            xch.send(i, c, A, Bf)
+                stepper.kick_slice(spec, lay, seed, traj, p, pre, n_global, slice_bits if chunked
+                                   else 0, sl, A)
+            xch.send(sl, A, Bf)
         xch.finish()
         lay = lay.exchanged()
         post = post_bits if p < P else 0

@@ -28,6 +28,11 @@ def _row_matrix(row):
 
 
 class NumpyShardStepper:
+    # slices of a single amplitude are fine here (the engine needs >= 12 index
+    # bits per slice: one 4096-amplitude tile), so small test states exercise
+    # the sliced exchange of sharded_forward_pipelined
+    min_slice_index_bits = 1
+
     def __init__(self, groups=None):
         self._groups = groups
 
@@ -120,19 +125,21 @@ class NumpyShardStepper:
         return obs
 
     # -- the asynchronous interface of sharded_forward_pipelined (synchronous here) --
-    def kick_chunk(self, spec, layout, seed, traj, period, pre, chunk_bits, chunk, buf):
-        """K_period on the local bits ``pre`` of chunk ``chunk`` (top chunk_bits
-        local bits) of every shard held, in place (dtc_shard_kick_chunk)."""
+    def kick_slice(self, spec, layout, seed, traj, period, pre, chunk_bits, slice_bits, slice_,
+                   buf):
+        """K_period on the local bits ``pre`` of slice ``slice_`` of every chunk
+        (top chunk_bits local bits; the next slice_bits number the slices) of
+        every shard held, in place (dtc_shard_kick_slice)."""
         nl = layout.n_local
-        nsub = nl - chunk_bits
+        nsub = nl - chunk_bits - slice_bits
         if pre >> nsub:
-            raise ValueError("chunk kick mask reaches the chunk bits")
-        psi = buf.numpy().reshape(layout.n_shards, -1)
-        sub = psi[:, chunk << nsub:(chunk + 1) << nsub].copy()
+            raise ValueError("slice kick mask reaches the chunk/slice bits")
+        psi = buf.numpy().reshape(layout.n_shards << chunk_bits, 1 << slice_bits, 1 << nsub)
+        sub = psi[:, slice_, :].copy()
         for q in range(nsub):
             if (pre >> q) & 1:
                 self._apply(sub, nsub, q, self._kick(spec, period, layout.site_of[q], seed, traj))
-        psi[:, chunk << nsub:(chunk + 1) << nsub] = sub
+        psi[:, slice_, :] = sub
 
     def step_async(self, spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
                    obs_out):

@@ -66,7 +66,7 @@ def test_l30_eight_virtual_ranks(pkg, engine, stepper):
 ])
 def test_pipelined_virtual_shards_match_engine(pkg, engine, stepper, L, k, T, p, state, pol,
                                                toff):
-    """The production C5 driver: per-chunk kicks (dtc_shard_kick_chunk), chunk
+    """The production C5 driver: per-slice kicks (dtc_shard_kick_slice), slice
     transfers on a side stream ordered by events, asynchronous fused steps with
     device observables (dtc_shard_step_async) -- same values as dtc_autocorr."""
     rng = np.random.default_rng(L * 11 + k)

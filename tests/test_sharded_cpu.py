@@ -79,6 +79,8 @@ def test_virtual_ranks_match_oracle(pkg, L, k, T, p, state, pol, toff, groups):
     (6, 1, 6, 0.0, "vacuum", "x", 0),
     (7, 2, 6, 0.1, "neel", "circular_left", 0),
     (9, 3, 5, 0.05, "neel", "xy", 1),
+    (10, 2, 4, 0.1, "vacuum", "x", 0),    # 4 slices per chunk
+    (11, 1, 4, 0.05, "neel", "y", 0),     # 8 slices per chunk
 ])
 @pytest.mark.parametrize("groups", [None, _halves])
 def test_pipelined_virtual_ranks_match_oracle(pkg, L, k, T, p, state, pol, toff, groups):
