@@ -569,11 +569,11 @@ def main_c4(args):
 
 def main_c5(args):
     """one noiseless state, L=34, tf=30, sharded over 8 ranks
-    (32 GiB per GPU): per period the pre-exchange kicks run chunk by chunk and
-    each chunk's transfer to its destination rank (RCCL point-to-point over
-    xGMI, side stream) starts while the next chunk is kicked; the fused pass
-    (kicks of the newly local sites, RZZ/RZ, <Z_i>, next kick) follows
-    (sharded.sharded_forward_pipelined).  On one GPU the same driver runs
+    (32 GiB per GPU): per period the pre-exchange kicks run slice by slice (slice
+    s of every destination chunk in one launch) and slice s travels to all 7
+    peers at once (RCCL point-to-point over xGMI, side stream) while slice s+1
+    is kicked; the fused pass (kicks of the newly local sites, RZZ/RZ, <Z_i>,
+    next kick) follows (sharded.sharded_forward_pipelined).  On one GPU the same driver runs
     2^shard_bits virtual ranks (default L=31 there; the transfers are device
     copies)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -653,7 +653,7 @@ def main_c5(args):
                                 f"<Z_i(t)> every period, {W} shards "
                                 f"({'virtual, 1 GPU' if world == 1 else 'one per GPU'})"),
                    "L": L, "tf": T, "shards": W, "parallelism": f"state-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "all pass kernels (chunk kicks / K-D-K), per-rank shard",
+        "roofline": {"bound": "hbm", "kernel": "all pass kernels (slice kicks / K-D-K), per-rank shard",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None},
         "period_ms": elapsed / (args.steps * P) * 1e3,
@@ -661,10 +661,11 @@ def main_c5(args):
         "exchange": {"per_period_ms": per_ex * 1e3,
                      "bytes_per_period_per_rank": sent,
                      "GBps_per_rank": sent / per_ex / 1e9 if per_ex > 0 else None,
-                     "window": ("side-stream events from the first chunk's transfer to the last "
-                                "one's completion (overlaps the chunk kicks)"),
-                     "kind": ("strided device copy per chunk (virtual ranks)" if world == 1 else
-                              "RCCL point-to-point per chunk over xGMI (isend/irecv pairs)")},
+                     "window": ("side-stream events from the first slice's transfer to the last "
+                                "one's completion (overlaps the slice kicks)"),
+                     "kind": ("strided device copy per slice (virtual ranks)" if world == 1 else
+                              "RCCL point-to-point per slice over xGMI: every peer at once "
+                              "(batch_isend_irecv of 7 sends + 7 receives)")},
         "pass_time_frac": ms / 1e3 / elapsed,
         "z_t1_mean": float(out["zsite"][1].mean()),
         "kat_cos_pi_g": float(np.cos(np.pi * 0.97)),
