@@ -310,7 +310,18 @@ struct PassSpec {
   KickDesc pre, post;
   int diag;    // DiagMode
   int d_index; // diagonals applied after this pass (valid when diag)
+  // light-cone end of an echo chain (kShapeLC): tile = bits 0..7 + sites
+  // lc_w0..lc_w0+3; pre D post D third on those sites, then the probe
+  int lc_w0 = -1;
+  KickDesc third = KickDesc{0, 0, 0, 0u, 0u, 0u};
+  int third_bits = 0;
 };
+
+// The tile geometry of a pass (the plan's group, or the light-cone window).
+Group pass_group(const Plan& pl, const PassSpec& ps) {
+  if (ps.lc_w0 >= 0) return Group{8, ps.lc_w0, 0xF00};
+  return pl.groups[ps.group];
+}
 
 // Emit the next pass of a chain (greedy, deterministic).
 PassSpec next_pass(Chain& ch) {
@@ -395,6 +406,7 @@ int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* 
 
 // Shape and matrix family of a pass.
 int pass_shape(const PassSpec& ps) {
+  if (ps.lc_w0 >= 0) return dtc::kShapeLC;
   const bool has_d = ps.diag != dtc::kDiagNone;
   if (ps.pre.enabled && has_d && ps.post.enabled) return dtc::kShapeKDK;
   if (ps.pre.enabled && has_d) return dtc::kShapeKD;
@@ -406,7 +418,7 @@ int pass_shape(const PassSpec& ps) {
 
 int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
   int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
-  for (const KickDesc* k : {&ps.pre, &ps.post}) {
+  for (const KickDesc* k : {&ps.pre, &ps.post, &ps.third}) {
     if (!k->enabled) continue;
     const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
     int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
@@ -420,10 +432,12 @@ int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
 }
 
 dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
-  const Group& g = rc.pl.groups[ps.group];
+  const Group g = pass_group(rc.pl, ps);
   dtc::PassKick pk{};
   pk.pre = ps.pre;
   pk.post = ps.post;
+  pk.third = ps.third;
+  pk.third_bits = ps.third_bits;
   pk.kind = pass_kind(rc, ps, pass_shape(ps));
   pk.c = g.c;
   pk.s = g.s;
@@ -453,7 +467,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     recs = P.out;
   }
   dtc::PassArgs A = base_args(ctx, rc, batch_start);
-  const Group& g = rc.pl.groups[ps.group];
+  const Group g = pass_group(rc.pl, ps);
 #ifdef DTC_PHASE_TIMING
   if (const char* e = std::getenv("DTC_DBG_GROUP"))
     if (std::atoi(e) != ps.group) A.dbg_ts = nullptr;
@@ -497,7 +511,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     const int nibs = ((g.act & 0xF) ? 1 : 0) | ((g.act & 0xF0) ? 2 : 0) | ((g.act & 0xF00) ? 4 : 0);
     const int io = dtc::io_layout(nibs), o = 3 - io;
     const bool n0 = nibs & 1, n_o = (nibs >> o) & 1;
-    const bool pre = shape == dtc::kShapeK || shape == dtc::kShapeKD || shape == dtc::kShapeKDK;
+    const bool pre = shape == dtc::kShapeK || shape == dtc::kShapeKD || shape == dtc::kShapeKDK ||
+                     shape == dtc::kShapeLC;
     const int tb = 4 * (pre ? (n_o ? o : (n0 ? 0 : io)) : io);
     if (!(tb >= g.c || tb + 4 <= g.c))
       return fail(DTC_EINVAL, "internal: diagonal nibble straddles the column bits");
@@ -1067,6 +1082,8 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       DTC_HIP(hipMemsetAsync(ctx->vals_e.p, 0, (size_t)nb * T * 2 * sizeof(double),
                              ctx->stream));
 
+    // DTC_NO_LIGHTCONE=1: keep the chains' last two passes (development A/B)
+    const bool lc_enabled = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
     // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
     // and branch the echo at t off F.  The whole batch schedule is built first.
     std::vector<Launch> sched;
@@ -1111,6 +1128,52 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
           const bool kick_only = l.ps.diag == dtc::kDiagNone && !l.ps.post.enabled;
           if (kick_only && !((group_bits(pl.groups[l.ps.group]) >> pr->probe_site) & 1ull))
             sched.pop_back();
+        }
+        // Light cone of <Z_j> through the chain's last three kick layers
+        // X_{n-2}, X_{n-1}, X_n (unitary kicks; D is diagonal): X_n matters
+        // only on j, X_{n-1} on j-1..j+1, X_{n-2} on j-2..j+2.  When the last
+        // two passes are [B: X_{n-2,B} D* X_{n-1,B}] [A: X_{n-1,A} D* X_{n,A}]
+        // (A = the probe's group) and those sites fit one 4-site window, one
+        // measure-only pass over a tile holding the window replaces both:
+        // X_{n-2} on the window's B sites, D*, X_{n-1}, D*, X_n on j.
+        if (!rc.device && lc_enabled && pl.groups.size() == 2 && sched.size() - chain0 >= 2) {
+          const PassSpec& p1 = sched[sched.size() - 2].ps;
+          const PassSpec& p2 = sched.back().ps;
+          const int j = pr->probe_site;
+          const int ga = ((group_bits(pl.groups[0]) >> j) & 1ull) ? 0 : 1;
+          auto same_layer = [](const KickDesc& a, const KickDesc& b) {
+            return a.enabled && b.enabled && a.row == b.row && a.mode == b.mode &&
+                   a.stream == b.stream && a.rng_period == b.rng_period;
+          };
+          if (p2.group == ga && p1.group != ga && p1.pre.enabled && p1.post.enabled &&
+              p1.diag == dtc::kDiagConj && p2.diag == dtc::kDiagConj && p2.pre.enabled &&
+              p2.post.enabled && same_layer(p1.post, p2.pre)) {
+            const uint64_t gb = group_bits(pl.groups[p1.group]);
+            uint64_t s1 = 0, s2 = 0;
+            for (int i = std::max(0, j - 2); i <= std::min(L - 1, j + 2); ++i)
+              if ((gb >> i) & 1ull) s1 |= 1ull << i;
+            for (int i = std::max(0, j - 1); i <= std::min(L - 1, j + 1); ++i) s2 |= 1ull << i;
+            const uint64_t u = s1 | s2 | (1ull << j);
+            const int lo = __builtin_ctzll(u), hi = 63 - __builtin_clzll(u);
+            int w0 = std::min(lo, L - 4);
+            if (hi - lo <= 3 && w0 >= 8 && w0 + 3 >= hi && w0 <= lo) {
+              PassSpec lc{p2.group, p1.pre, p2.pre, dtc::kDiagConj, p2.d_index};
+              lc.lc_w0 = w0;
+              lc.third = p2.post;
+              uint32_t sk1 = 0, sk2 = 0;
+              for (int q = 0; q < 4; ++q) {
+                if (!((s1 >> (w0 + q)) & 1ull)) sk1 |= 1u << (8 + q);
+                if (!((s2 >> (w0 + q)) & 1ull)) sk2 |= 1u << (8 + q);
+              }
+              lc.pre.skip = sk1;
+              lc.post.skip = sk2;
+              lc.third_bits = 1 << (j - w0);
+              const Launch first = sched[sched.size() - 2];
+              sched.pop_back();
+              sched.back() = Launch{lc, first.src, first.dst, dtc::kMeasProbe, 1, 2, nullptr,
+                                    (int64_t)T * 2};
+            }
+          }
         }
         sched.back().meas_mode = dtc::kMeasProbe;
         sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;

@@ -49,7 +49,11 @@ enum MeasMode {
 // the time the engine assigns them to (dtc_energy).
 enum MeasPart { kPartZ = 1, kPartXPost = 2, kPartXPre = 4 };
 // Which parts a pass runs: pre-kick (K), diagonal (D), post-kick (K).
-enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4 };
+// kShapeLC: the light-cone end of an echo chain (measure-only, one 4-site
+// register nibble = sites w0..w0+3 at tile bits 8..11): pre-kick, D, post-kick,
+// D, third kick (records in the pre slots of tile bits 0..3), probe.
+enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4,
+                 kShapeLC = 5 };
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
@@ -97,6 +101,8 @@ struct PassKick {
   KickDesc pre, post;   // enabled = 0: no such layer
   int kind;             // KickKind of the pass
   int c, s, act;        // tile geometry (see PassArgs)
+  KickDesc third;       // kShapeLC: the third kick layer, on tile bits 8 + q for the
+  int third_bits;       // bits q of third_bits; records in the pre slots q (0..3)
 };
 
 struct PrepArgs {

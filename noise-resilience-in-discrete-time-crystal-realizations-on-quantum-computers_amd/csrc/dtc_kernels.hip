@@ -265,6 +265,13 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
         const int site = P.site_of ? P.site_of[lsite] : lsite;
         build_site_kick(P, K, site, traj, m);
       }
+      if (half == 0 && k < 4 && pk.third.enabled && ((pk.third_bits >> k) & 1)) {
+        // light-cone pass: the third layer on tile bit 8 + k, in pre slot k
+        const int tb = 8 + k;
+        const int tsite = tb < pk.c ? tb : pk.s + tb - pk.c;
+        if (tsite < P.L_real) build_site_kick(P, pk.third, P.site_of ? P.site_of[tsite] : tsite,
+                                              traj, m);
+      }
       SiteMat sm;
       canonicalise(pk.kind, m, sm);
       KickRec r;
@@ -602,10 +609,11 @@ struct RoundPlan {
   static constexpr int IO = io_layout(NIBS);
   static constexpr int O = 3 - IO;
   static constexpr bool n0 = NIBS & 1, nIO = (NIBS >> IO) & 1, nO = (NIBS >> O) & 1;
-  static constexpr bool pre = SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK;
-  static constexpr bool diag =
-      SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeD;
-  static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK;
+  static constexpr bool pre =
+      SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK || SHAPE == kShapeLC;
+  static constexpr bool diag = SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK ||
+                               SHAPE == kShapeD || SHAPE == kShapeLC;
+  static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeLC;
   static constexpr int d_lay = pre ? (nO ? O : (n0 ? 0 : IO)) : IO;
   // layouts reached by the post rounds
   static constexpr int pO = nO ? O : d_lay;
@@ -744,7 +752,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const double2 gph = make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1));
   const double inv_w2_mid = R.d(kRecTotal, 2);
 
-  auto diag_in = [&](auto lay_tag) {
+  auto diag_in = [&](auto lay_tag, bool with_g) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
     // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
@@ -753,8 +761,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     // nibble of layout LAY inside or outside the column bits: g0 >= 0)
     const int w0i = (int)(((x0 << 1) >> g0) & 63);
     const double2 w0 = s_win[w0i];
-    const double2 pc =
-        cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+    const double2 pc = cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)),
+                            with_g ? gph : make_double2(1.0, 0.0));
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
   };
@@ -1002,7 +1010,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   // ---- diagonal and measurement at d_lay ----
   using DL = std::integral_constant<int, RP::d_lay>;
-  if constexpr (RP::diag) diag_in(DL{});
+  if constexpr (RP::diag) diag_in(DL{}, true);
   if constexpr (MC > 0) {
     if (A.meas != kMeasNone && !A.meas_at_end &&
         (A.meas != kMeasEnergy || (A.meas_parts & kPartZ)))
@@ -1032,6 +1040,13 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
     exchange<RP::pIO, RP::IO>(v, s_tile, t);
+    if constexpr (SHAPE == kShapeLC) {
+      // the chain's last diagonal and the probe site's last kick (one nibble:
+      // everything stays in the IO layout's registers)
+      static_assert(NIBS == 4, "light-cone pass: one register nibble");
+      diag_in(LIO{}, false);
+      apply_nibble<RP::IO, KIND>(v, R, -4 * RP::IO);
+    }
   } else {
     exchange<RP::d_lay, RP::IO>(v, s_tile, t);
   }
@@ -1128,6 +1143,7 @@ DTC_DEFINE_FINAL(dtc_kdk_final, kShapeKDK)
 DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
 DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
 DTC_DEFINE_FINAL(dtc_kick_final, kShapeK)
+DTC_DEFINE_FINAL(dtc_lc_final, kShapeLC)
 #undef DTC_DEFINE_FINAL
 template <int NIBS, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
@@ -1146,6 +1162,13 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
         case kShapeKD: hipLaunchKernelGGL((dtc_kd_final<NIBS, KIND>), grid, block, 0, stream, a); break;
         case kShapeDK: hipLaunchKernelGGL((dtc_dk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
         case kShapeK: hipLaunchKernelGGL((dtc_kick_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        case kShapeLC:
+          if constexpr (NIBS == 4) {
+            hipLaunchKernelGGL((dtc_lc_final<NIBS, KIND>), grid, block, 0, stream, a);
+            break;
+          } else {
+            return hipErrorInvalidValue;
+          }
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();

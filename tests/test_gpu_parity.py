@@ -185,3 +185,27 @@ def test_noise_sampler_unbiased_high_resolution(pkg, engine):
     m, se = echo1.mean(), echo1.std() / np.sqrt(n)
     assert abs(m - (1 - p) ** 8) < 4.5 * se, (m, (1 - p) ** 8, se)
     assert se / (1 - p) ** 8 < 5e-4
+
+
+@pytest.mark.parametrize("L,T,p,state,pol,toff", [
+    (20, 7, 0.1, "vacuum", "x", 0),
+    (20, 6, 0.05, "neel", "xy", 1),
+    (21, 6, 0.1, "vacuum", "circular_left", 0),
+    (21, 5, 0.0, "vacuum", "y", 0),
+])
+def test_echo_light_cone_end(pkg, engine, monkeypatch, L, T, p, state, pol, toff):
+    """Echo chains ending in the light-cone pass (the last two passes merged into
+    one measure-only pass over sites j-1..j+2 with the kicks outside the light
+    cone of Z_j dropped): the same per-trajectory echo as the oracle (1e-10) and
+    as the engine without the merge (DTC_NO_LIGHTCONE=1)."""
+    rng = np.random.default_rng(L * 31 + T)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    got = engine.autocorr(spec, 3, seed=77)
+    ref = c_oracle.autocorr(spec, 3, seed=77)
+    _cmp(got, ref)
+    monkeypatch.setenv("DTC_NO_LIGHTCONE", "1")
+    full = engine.autocorr(spec, 3, seed=77)
+    assert np.abs(got["echo"] - full["echo"]).max() < 1e-12
+    assert np.abs(got["fwd"] - full["fwd"]).max() == 0.0
