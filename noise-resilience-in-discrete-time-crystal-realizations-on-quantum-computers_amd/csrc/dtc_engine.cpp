@@ -310,16 +310,18 @@ struct PassSpec {
   KickDesc pre, post;
   int diag;    // DiagMode
   int d_index; // diagonals applied after this pass (valid when diag)
-  // light-cone end of an echo chain (kShapeLC): tile = bits 0..7 + sites
-  // lc_w0..lc_w0+3; pre D post D third on those sites, then the probe
+  // light-cone end of an echo chain (kShapeLC): tile = bits 0..3 + sites
+  // lc_w0..lc_w0+7; layers lc[0] D* lc[1] ... D* lc[lc_layers-1] on the window
+  // sites of lc_mask (bit 8 l + b: site lc_w0 + b in layer l), then the probe
   int lc_w0 = -1;
-  KickDesc third = KickDesc{0, 0, 0, 0u, 0u, 0u};
-  int third_bits = 0;
+  int lc_layers = 0;
+  KickDesc lc[dtc::kLcLayers] = {};
+  uint64_t lc_mask = 0;
 };
 
 // The tile geometry of a pass (the plan's group, or the light-cone window).
 Group pass_group(const Plan& pl, const PassSpec& ps) {
-  if (ps.lc_w0 >= 0) return Group{8, ps.lc_w0, 0xF00};
+  if (ps.lc_w0 >= 0) return Group{4, ps.lc_w0, 0xFF0};
   return pl.groups[ps.group];
 }
 
@@ -418,7 +420,10 @@ int pass_shape(const PassSpec& ps) {
 
 int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
   int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
-  for (const KickDesc* k : {&ps.pre, &ps.post, &ps.third}) {
+  std::vector<const KickDesc*> ks{&ps.pre, &ps.post};
+  for (int l = 0; l < ps.lc_layers; ++l)
+    if ((ps.lc_mask >> (dtc::kLcSites * l)) & 0xFFull) ks.push_back(&ps.lc[l]);
+  for (const KickDesc* k : ks) {
     if (!k->enabled) continue;
     const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
     int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
@@ -436,8 +441,9 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
   dtc::PassKick pk{};
   pk.pre = ps.pre;
   pk.post = ps.post;
-  pk.third = ps.third;
-  pk.third_bits = ps.third_bits;
+  pk.lc_layers = ps.lc_layers;
+  for (int l = 0; l < dtc::kLcLayers; ++l) pk.lc[l] = ps.lc[l];
+  pk.lc_mask = ps.lc_mask;
   pk.kind = pass_kind(rc, ps, pass_shape(ps));
   pk.c = g.c;
   pk.s = g.s;
@@ -529,6 +535,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.meas_at_end = meas_at_end;
   A.meas_parts = meas_parts;
   A.no_store = no_store;
+  A.lc_layers = ps.lc_layers;
+  A.lc_mask = ps.lc_mask;
   A.batch = batch;
   A.n_obs = n_obs;
   const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
@@ -779,6 +787,18 @@ uint64_t group_bits(const Group& g) {
   return m;
 }
 
+// The kick sites of layer `k` in a pass over group g (tile bits outside
+// k.skip), below L.
+uint64_t layer_sites(const Group& g, const KickDesc& k, int L) {
+  uint64_t m = 0;
+  for (int b = 0; b < dtc::kTileBits; ++b) {
+    if (!(g.act & ~(int)k.skip & (1 << b))) continue;
+    const int site = b < g.c ? b : g.s + b - g.c;
+    if (site < L) m |= 1ull << site;
+  }
+  return m;
+}
+
 // tile bits of group g that are NOT in mask (left identity by a kick layer)
 uint32_t skip_bits(const Group& g, uint64_t mask) {
   uint32_t sk = 0;
@@ -788,6 +808,77 @@ uint32_t skip_bits(const Group& g, uint64_t mask) {
     if (!((mask >> bit) & 1)) sk |= 1u << k;
   }
   return sk;
+}
+
+// Light-cone end of the echo chain sched[chain0 ..) measuring Z_j: replace
+// its last k passes (k = 4 .. 2, the first that fits) by one kShapeLC pass.
+// The passes' kicks and diagonals, in order, form layers separated by the
+// D*'s; layer l of M (r = M - 1 - l diagonals before the probe) only matters
+// on sites j-r .. j+r, and the layers' remaining sites must fit one 8-site
+// window w0 .. w0+7 (4 <= w0 <= L - 8: clear of tile bits 0..3).
+void lc_merge(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j) {
+  const Plan& pl = rc.pl;
+  const int L = pl.L;
+  auto same_layer = [](const KickDesc& a, const KickDesc& b) {
+    return a.row == b.row && a.mode == b.mode && a.stream == b.stream &&
+           a.rng_period == b.rng_period;
+  };
+  const int n_chain = (int)(sched.size() - chain0);
+  for (int k = std::min(4, n_chain); k >= 2; --k) {
+    std::vector<KickDesc> desc(1, no_kick());
+    std::vector<uint64_t> sites(1, 0);
+    bool ok = true;
+    int pending_d = 0;  // diagonals not yet followed by a kick (trailing ones are dropped)
+    auto kick = [&](const Group& g, const KickDesc& kd) {
+      for (; pending_d > 0; --pending_d) {
+        desc.push_back(no_kick());
+        sites.push_back(0);
+      }
+      if (desc.back().enabled && !same_layer(desc.back(), kd)) ok = false;
+      desc.back() = kd;
+      desc.back().skip = 0;
+      sites.back() |= layer_sites(g, kd, L);
+    };
+    for (size_t i = sched.size() - k; i < sched.size(); ++i) {
+      const PassSpec& ps = sched[i].ps;
+      if (ps.lc_w0 >= 0) ok = false;
+      if (!ok) break;
+      const Group& g = pl.groups[ps.group];
+      if (ps.pre.enabled) kick(g, ps.pre);
+      if (ps.diag != dtc::kDiagNone) {
+        if (ps.diag != dtc::kDiagConj) ok = false;
+        ++pending_d;
+      }
+      if (ps.post.enabled) kick(g, ps.post);
+    }
+    const int M = (int)desc.size();
+    if (!ok || M > dtc::kLcLayers) continue;
+    uint64_t u = 1ull << j;
+    for (int l = 0; l < M; ++l) {
+      const int r = M - 1 - l;
+      uint64_t cone = 0;
+      for (int i = std::max(0, j - r); i <= std::min(L - 1, j + r); ++i) cone |= 1ull << i;
+      sites[l] &= cone;
+      u |= sites[l];
+    }
+    const int lo = __builtin_ctzll(u), hi = 63 - __builtin_clzll(u);
+    const int w0 = std::max(4, std::min(lo, L - 8));
+    if (w0 > lo || hi > w0 + 7 || w0 + 8 > pl.L_eff) continue;
+    const PassSpec& last = sched.back().ps;
+    PassSpec lc{last.group, no_kick(), no_kick(), dtc::kDiagConj, last.d_index};
+    lc.lc_w0 = w0;
+    lc.lc_layers = M;
+    for (int l = 0; l < M; ++l) {
+      lc.lc[l] = desc[l];
+      lc.lc_mask |= ((sites[l] >> w0) & 0xFFull) << (dtc::kLcSites * l);
+    }
+    const int kind = pass_kind(rc, lc, dtc::kShapeLC);
+    if (kind != dtc::kKindRX && kind != dtc::kKindRY) continue;
+    const Launch first = sched[sched.size() - k];
+    sched.resize(sched.size() - k + 1);
+    sched.back() = Launch{lc, first.src, first.dst, dtc::kMeasProbe, 1, 2, nullptr, first.meas_stride};
+    return;
+  }
 }
 }  // namespace
 
@@ -1129,52 +1220,15 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
           if (kick_only && !((group_bits(pl.groups[l.ps.group]) >> pr->probe_site) & 1ull))
             sched.pop_back();
         }
-        // Light cone of <Z_j> through the chain's last three kick layers
-        // X_{n-2}, X_{n-1}, X_n (unitary kicks; D is diagonal): X_n matters
-        // only on j, X_{n-1} on j-1..j+1, X_{n-2} on j-2..j+2.  When the last
-        // two passes are [B: X_{n-2,B} D* X_{n-1,B}] [A: X_{n-1,A} D* X_{n,A}]
-        // (A = the probe's group) and those sites fit one 4-site window, one
-        // measure-only pass over a tile holding the window replaces both:
-        // X_{n-2} on the window's B sites, D*, X_{n-1}, D*, X_n on j.
-        if (!rc.device && lc_enabled && pl.groups.size() == 2 && sched.size() - chain0 >= 2) {
-          const PassSpec& p1 = sched[sched.size() - 2].ps;
-          const PassSpec& p2 = sched.back().ps;
-          const int j = pr->probe_site;
-          const int ga = ((group_bits(pl.groups[0]) >> j) & 1ull) ? 0 : 1;
-          auto same_layer = [](const KickDesc& a, const KickDesc& b) {
-            return a.enabled && b.enabled && a.row == b.row && a.mode == b.mode &&
-                   a.stream == b.stream && a.rng_period == b.rng_period;
-          };
-          if (p2.group == ga && p1.group != ga && p1.pre.enabled && p1.post.enabled &&
-              p1.diag == dtc::kDiagConj && p2.diag == dtc::kDiagConj && p2.pre.enabled &&
-              p2.post.enabled && same_layer(p1.post, p2.pre)) {
-            const uint64_t gb = group_bits(pl.groups[p1.group]);
-            uint64_t s1 = 0, s2 = 0;
-            for (int i = std::max(0, j - 2); i <= std::min(L - 1, j + 2); ++i)
-              if ((gb >> i) & 1ull) s1 |= 1ull << i;
-            for (int i = std::max(0, j - 1); i <= std::min(L - 1, j + 1); ++i) s2 |= 1ull << i;
-            const uint64_t u = s1 | s2 | (1ull << j);
-            const int lo = __builtin_ctzll(u), hi = 63 - __builtin_clzll(u);
-            int w0 = std::min(lo, L - 4);
-            if (hi - lo <= 3 && w0 >= 8 && w0 + 3 >= hi && w0 <= lo) {
-              PassSpec lc{p2.group, p1.pre, p2.pre, dtc::kDiagConj, p2.d_index};
-              lc.lc_w0 = w0;
-              lc.third = p2.post;
-              uint32_t sk1 = 0, sk2 = 0;
-              for (int q = 0; q < 4; ++q) {
-                if (!((s1 >> (w0 + q)) & 1ull)) sk1 |= 1u << (8 + q);
-                if (!((s2 >> (w0 + q)) & 1ull)) sk2 |= 1u << (8 + q);
-              }
-              lc.pre.skip = sk1;
-              lc.post.skip = sk2;
-              lc.third_bits = 1 << (j - w0);
-              const Launch first = sched[sched.size() - 2];
-              sched.pop_back();
-              sched.back() = Launch{lc, first.src, first.dst, dtc::kMeasProbe, 1, 2, nullptr,
-                                    (int64_t)T * 2};
-            }
-          }
-        }
+        // Light cone of <Z_j> through the chain's last kick layers (unitary
+        // single-site kicks, D diagonal with nearest-neighbour couplings): the
+        // last layer X_n matters only on j, X_{n-1} on j-1..j+1, X_{n-r} on
+        // j-r..j+r.  The chain's last k passes (k = 4 .. 2, the most that fit)
+        // become one measure-only pass over a tile holding the 8-site window
+        // of the kicks left: their layers, restricted to the cone, with D*
+        // between them, then the probe.
+        if (!rc.device && lc_enabled && sched.size() - chain0 >= 2)
+          lc_merge(rc, sched, chain0, pr->probe_site);
         sched.back().meas_mode = dtc::kMeasProbe;
         sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;
         // the echo state is only measured: the chain's last pass reads its

@@ -49,11 +49,18 @@ enum MeasMode {
 // the time the engine assigns them to (dtc_energy).
 enum MeasPart { kPartZ = 1, kPartXPost = 2, kPartXPre = 4 };
 // Which parts a pass runs: pre-kick (K), diagonal (D), post-kick (K).
-// kShapeLC: the light-cone end of an echo chain (measure-only, one 4-site
-// register nibble = sites w0..w0+3 at tile bits 8..11): pre-kick, D, post-kick,
-// D, third kick (records in the pre slots of tile bits 0..3), probe.
+// kShapeLC: the light-cone end of an echo chain (lc_body in dtc_kernels.hip):
+// up to kLcLayers kick layers with D between them on the 8-site window at
+// tile bits 4..11 (c = 4), each layer only on the sites its mask keeps, then
+// the probe; measure-only (no store).
 enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD = 4,
                  kShapeLC = 5 };
+static constexpr int kLcLayers = 5;
+static constexpr int kLcSites = 8;
+// LC records (compact, in the state's KickRec block read as doubles): layer l,
+// window site b -> doubles 2 (8 l + b) (coefficient) and + 1 (variant, as
+// integer); the global factor at doubles kLcTotal, kLcTotal + 1.
+static constexpr int kLcTotal = 2 * kLcLayers * kLcSites;
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
@@ -101,8 +108,9 @@ struct PassKick {
   KickDesc pre, post;   // enabled = 0: no such layer
   int kind;             // KickKind of the pass
   int c, s, act;        // tile geometry (see PassArgs)
-  KickDesc third;       // kShapeLC: the third kick layer, on tile bits 8 + q for the
-  int third_bits;       // bits q of third_bits; records in the pre slots q (0..3)
+  int lc_layers;        // kShapeLC: layers lc[0 .. lc_layers), site b of layer l kicked
+  KickDesc lc[kLcLayers];  // when bit 8 l + b of lc_mask is set (window site b = tile
+  uint64_t lc_mask;     // bit 4 + b); compact records (kLcTotal)
 };
 
 struct PrepArgs {
@@ -164,6 +172,8 @@ struct PassArgs {
   int n_obs;               // kMeasProbe: 2; kMeasSites: 1 + L_real; kMeasEnergy: 4 L_real
   int meas_parts;          // kMeasEnergy: MeasPart bits
   int no_store;            // measure only: the tile is not written back (dst unused)
+  int lc_layers;           // kShapeLC: kick layers; lc_mask bit 8 l + b = site b of layer l
+  uint64_t lc_mask;
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]

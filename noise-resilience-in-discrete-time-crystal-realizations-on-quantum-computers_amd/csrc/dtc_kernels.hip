@@ -253,6 +253,32 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   const int64_t gstate = P.batch_start + b;
   const uint64_t traj = (uint64_t)(P.traj_offset + (gstate % P.n_traj));
   KickRec* out = P.out + id * kRecPerState;
+  if (pk.lc_layers > 0) {
+    // light-cone pass: compact records of the masked (layer, window site) kicks
+    double* od = (double*)out;
+    long long* oi = (long long*)out;
+    int ks = 0;
+    double wl = 1.0;
+    for (int l = 0; l < pk.lc_layers; ++l)
+      for (int b = 0; b < kLcSites; ++b) {
+        if (!((pk.lc_mask >> (kLcSites * l + b)) & 1ull)) continue;
+        const int lsite = pk.s + b;  // tile bit 4 + b >= c = 4
+        double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0),
+                        make_double2(1.0, 0.0)};
+        if (lsite < P.L_real)
+          build_site_kick(P, pk.lc[l], P.site_of ? P.site_of[lsite] : lsite, traj, m);
+        SiteMat sm;
+        canonicalise(pk.kind, m, sm);
+        od[2 * (kLcSites * l + b)] = sm.coef;
+        oi[2 * (kLcSites * l + b) + 1] = sm.var;
+        ks += sm.k;
+        wl *= sm.scale;
+      }
+    const int kph = ks & 3;
+    od[kLcTotal] = kph == 0 ? wl : (kph == 2 ? -wl : 0.0);
+    od[kLcTotal + 1] = kph == 1 ? wl : (kph == 3 ? -wl : 0.0);
+    return;
+  }
   int ksum = 0;
   double w[2] = {1.0, 1.0};
   for (int half = 0; half < 2; ++half) {
@@ -265,13 +291,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
         const int site = P.site_of ? P.site_of[lsite] : lsite;
         build_site_kick(P, K, site, traj, m);
       }
-      if (half == 0 && k < 4 && pk.third.enabled && ((pk.third_bits >> k) & 1)) {
-        // light-cone pass: the third layer on tile bit 8 + k, in pre slot k
-        const int tb = 8 + k;
-        const int tsite = tb < pk.c ? tb : pk.s + tb - pk.c;
-        if (tsite < P.L_real) build_site_kick(P, pk.third, P.site_of ? P.site_of[tsite] : tsite,
-                                              traj, m);
-      }
+
       SiteMat sm;
       canonicalise(pk.kind, m, sm);
       KickRec r;
@@ -609,11 +629,10 @@ struct RoundPlan {
   static constexpr int IO = io_layout(NIBS);
   static constexpr int O = 3 - IO;
   static constexpr bool n0 = NIBS & 1, nIO = (NIBS >> IO) & 1, nO = (NIBS >> O) & 1;
-  static constexpr bool pre =
-      SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK || SHAPE == kShapeLC;
-  static constexpr bool diag = SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK ||
-                               SHAPE == kShapeD || SHAPE == kShapeLC;
-  static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeLC;
+  static constexpr bool pre = SHAPE == kShapeK || SHAPE == kShapeKD || SHAPE == kShapeKDK;
+  static constexpr bool diag =
+      SHAPE == kShapeKD || SHAPE == kShapeDK || SHAPE == kShapeKDK || SHAPE == kShapeD;
+  static constexpr bool post = SHAPE == kShapeDK || SHAPE == kShapeKDK;
   static constexpr int d_lay = pre ? (nO ? O : (n0 ? 0 : IO)) : IO;
   // layouts reached by the post rounds
   static constexpr int pO = nO ? O : d_lay;
@@ -1040,13 +1059,6 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
     exchange<RP::pIO, RP::IO>(v, s_tile, t);
-    if constexpr (SHAPE == kShapeLC) {
-      // the chain's last diagonal and the probe site's last kick (one nibble:
-      // everything stays in the IO layout's registers)
-      static_assert(NIBS == 4, "light-cone pass: one register nibble");
-      diag_in(LIO{}, false);
-      apply_nibble<RP::IO, KIND>(v, R, -4 * RP::IO);
-    }
   } else {
     exchange<RP::d_lay, RP::IO>(v, s_tile, t);
   }
@@ -1143,11 +1155,189 @@ DTC_DEFINE_FINAL(dtc_kdk_final, kShapeKDK)
 DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
 DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
 DTC_DEFINE_FINAL(dtc_kick_final, kShapeK)
-DTC_DEFINE_FINAL(dtc_lc_final, kShapeLC)
 #undef DTC_DEFINE_FINAL
 template <int NIBS, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
   pass_body<kShapeD, NIBS, kKindRX, MC>(A);
+}
+
+// ---- the light-cone end of an echo chain (kShapeLC) ------------------------
+// The chain ends with <Z_j>.  Going backward from the measurement, the last
+// kick layer matters only on j, the one before on j-1..j+1, the r-th from the
+// end on j-r..j+r (kicks are unitary and D is diagonal), so the chain's last
+// few passes collapse into one measure-only pass over tiles that hold the
+// window w0..w0+7 (tile bits 4..11; bits 0..3 = sites 0..3 as columns, c = 4):
+// layer l = 0 .. lc_layers-1 kicks the window sites its mask keeps -- nibble 2
+// then 1 for even l, 1 then 2 for odd l, one LDS re-layout between them --
+// with D (conjugated: echo) between consecutive layers; then the probe.
+// Compact records (kLcTotal): (layer, site) -> coefficient, variant.
+template <int KIND>
+__device__ __forceinline__ void lc_body(const PassArgs& A) {
+  static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
+  __shared__ double2 s_tile[kTile];
+  __shared__ double2 s_chunk[kMaxChunks * 64];
+  __shared__ double2 s_win[2][64];
+  __shared__ double s_red[kThreads / 64][2];
+  const int t = threadIdx.x;
+  const int c = A.c, s = A.s;  // c = 4, s = w0
+  const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
+  const int64_t b = blockIdx.y;
+  const int64_t tile = blockIdx.x;
+  const int inst = (int)((A.batch_start + b) / A.n_traj);
+  RecRegs R;
+  {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < kLcTotal + 2) {  // the compact records: lanes 0 .. 20
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
+  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
+  TileMap M;
+  M.c = c;
+  M.s = s;
+  M.cmask = (1 << c) - 1;
+  M.tbase = ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
+  // diagonal tables: chunks + the window tables of layouts 1 (g0 = s) and 2 (s + 4)
+  constexpr int kChunkPerThread = (kMaxChunks * 64 + kThreads - 1) / kThreads;
+  double2 dchunk[kChunkPerThread];
+  double2 dwin = make_double2(1.0, 0.0);
+  const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
+#pragma unroll
+  for (int j = 0; j < kChunkPerThread; ++j) {
+    const int i = t + j * kThreads;
+    if (i < A.n_chunks * 64) dchunk[j] = dt[i];
+  }
+  if (t < 128) dwin = dt[(A.n_chunks + s + 4 * (t >> 6)) * 64 + (t & 63)];
+  // the tile in layout 2 (threads = tile bits 0..7: 16-amplitude runs)
+  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
+  double2 v[kRegs];
+  {
+    const char* src = (const char*)(A.src + b * A.state_len);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const char* a = src + ((M.tbase | M.rel(r << 8)) << 4) + vofs;
+      const d2v w = __builtin_nontemporal_load((const d2v*)a);
+      v[r] = make_double2(w.x, w.y);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // tables landed, the tile's 16 loads in flight
+  const double cs = A.diag_conj ? -1.0 : 1.0;
+#pragma unroll
+  for (int j = 0; j < kChunkPerThread; ++j) {
+    const int i = t + j * kThreads;
+    if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
+  }
+  if (t < 128) s_win[t >> 6][t & 63] = make_double2(dwin.x, cs * dwin.y);
+  // (visible after the first re-layout's barrier)
+  // record (layer l, window site q) in the compact layout
+  auto coef = [&](int l, int q) { return R.d(0, 2 * (kLcSites * l + q)); };
+  auto var = [&](int l, int q) { return R.i(0, 2 * (kLcSites * l + q) + 1); };
+  // the kicks' global factor (a phase times the product of the real scales):
+  // only its modulus matters to the probe
+  const double g2 = fma(R.d(0, kLcTotal), R.d(0, kLcTotal), R.d(0, kLcTotal + 1) * R.d(0, kLcTotal + 1));
+
+  auto kick = [&](auto n_tag, auto l_tag) {
+    constexpr int N = decltype(n_tag)::value;  // nibble = layout in registers
+    constexpr int l = decltype(l_tag)::value;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int site = 4 * (N - 1) + q;  // window site of tile bit 4 N + q
+      if (!((A.lc_mask >> (kLcSites * l + site)) & 1ull)) continue;
+      const double f = coef(l, site);
+      const int vv = var(l, site);
+      auto run = [&](auto qtag) {
+        constexpr int Q = decltype(qtag)::value;
+        if (vv == 0) layer_f<KIND, 0, Q>(v, f);
+        else if (vv == 1) layer_f<KIND, 1, Q>(v, f);
+        else if (vv == 2) layer_f<KIND, 2, Q>(v, f);
+        else layer_f<KIND, 3, Q>(v, f);
+      };
+      if (q == 0) run(std::integral_constant<int, 0>{});
+      else if (q == 1) run(std::integral_constant<int, 1>{});
+      else if (q == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
+    }
+  };
+  auto diag = [&](auto lay_tag) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int g0 = s + 4 * LAY - c;  // the window of the nibble in registers
+    const double2* win = s_win[LAY - 1];
+    const int64_t x0 = M.at(ybase<LAY>(t));
+    const int w0i = (int)(((x0 << 1) >> g0) & 63);
+    const double2 w0 = win[w0i];
+    const double2 pc = cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y));
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, win[w0i | (r << 1)]));
+  };
+  using L1 = std::integral_constant<int, 1>;
+  using L2 = std::integral_constant<int, 2>;
+  const int nl = A.lc_layers;
+  // layer 0: nibble 2 (layout 2), re-layout, nibble 1 (layout 1), D
+  kick(L2{}, std::integral_constant<int, 0>{});
+  exchange<2, 1>(v, s_tile, t);
+  kick(L1{}, std::integral_constant<int, 0>{});
+  if (nl > 1) diag(L1{});
+  if (nl > 1) {  // layer 1: 1 -> 2
+    kick(L1{}, std::integral_constant<int, 1>{});
+    exchange<1, 2>(v, s_tile, t);
+    kick(L2{}, std::integral_constant<int, 1>{});
+    if (nl > 2) diag(L2{});
+  }
+  if (nl > 2) {  // layer 2: 2 -> 1
+    kick(L2{}, std::integral_constant<int, 2>{});
+    exchange<2, 1>(v, s_tile, t);
+    kick(L1{}, std::integral_constant<int, 2>{});
+    if (nl > 3) diag(L1{});
+  }
+  if (nl > 3) {  // layer 3: 1 -> 2
+    kick(L1{}, std::integral_constant<int, 3>{});
+    exchange<1, 2>(v, s_tile, t);
+    kick(L2{}, std::integral_constant<int, 3>{});
+    if (nl > 4) diag(L2{});
+  }
+  if (nl > 4) {  // layer 4: 2 -> 1
+    kick(L2{}, std::integral_constant<int, 4>{});
+    exchange<2, 1>(v, s_tile, t);
+    kick(L1{}, std::integral_constant<int, 4>{});
+  }
+  // probe: layout 1 after an odd number of layers, 2 after an even number
+  const int lay = (nl & 1) ? 1 : 2;
+  double ptot = 0.0, pz = 0.0;
+  {
+    const int64_t x0 = lay == 1 ? M.at(ybase<1>(t)) : M.at(ybase<2>(t));
+    const int site = A.probe;
+    const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+    const int jr = tb - 4 * lay;  // register bit of the probe, if in the nibble in registers
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+      ptot += p2;
+      pz += (jr >= 0 && jr < 4 && ((r >> jr) & 1)) ? -p2 : p2;
+    }
+    if (!(jr >= 0 && jr < 4)) pz = ((x0 >> site) & 1) ? -ptot : ptot;
+  }
+  const int wave = t >> 6, lane = t & 63;
+  const double tot = wave_sum(ptot) * g2;
+  const double z = wave_sum(pz) * g2;
+  if (lane == 0) {
+    s_red[wave][0] = tot;
+    s_red[wave][1] = z;
+  }
+  __syncthreads();
+  if (t < 2) {
+    double acc = 0.0;
+    for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
+    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_lc_final(PassArgs A) {
+  lc_body<KIND>(A);
 }
 
 template <int NIBS, int KIND, int MC>
@@ -1162,13 +1352,6 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
         case kShapeKD: hipLaunchKernelGGL((dtc_kd_final<NIBS, KIND>), grid, block, 0, stream, a); break;
         case kShapeDK: hipLaunchKernelGGL((dtc_dk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
         case kShapeK: hipLaunchKernelGGL((dtc_kick_final<NIBS, KIND>), grid, block, 0, stream, a); break;
-        case kShapeLC:
-          if constexpr (NIBS == 4) {
-            hipLaunchKernelGGL((dtc_lc_final<NIBS, KIND>), grid, block, 0, stream, a);
-            break;
-          } else {
-            return hipErrorInvalidValue;
-          }
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1229,6 +1412,19 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
     return hipErrorInvalidValue;
   const int n_tiles = 1 << (a.L_eff - kTileBits);
   dim3 grid(n_tiles, batch);
+  if (shape == kShapeLC) {
+    // measure-only light-cone pass: probe, window at tile bits 4..11 (c = 4)
+    if (a.c != 4 || a.act != 0xFF0 || a.meas != kMeasProbe || !a.no_store || a.lc_layers < 1 ||
+        a.lc_layers > kLcLayers || a.n_obs < 2)
+      return hipErrorInvalidValue;
+    if (kind == kKindRX)
+      hipLaunchKernelGGL((dtc_lc_final<kKindRX>), grid, dim3(kThreads), 0, stream, a);
+    else if (kind == kKindRY)
+      hipLaunchKernelGGL((dtc_lc_final<kKindRY>), grid, dim3(kThreads), 0, stream, a);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   int nibs = 0;
   for (int n = 0; n < 3; ++n)
     if (a.act & (0xF << (4 * n))) nibs |= 1 << n;

@@ -187,21 +187,27 @@ def test_noise_sampler_unbiased_high_resolution(pkg, engine):
     assert se / (1 - p) ** 8 < 5e-4
 
 
-@pytest.mark.parametrize("L,T,p,state,pol,toff", [
-    (20, 7, 0.1, "vacuum", "x", 0),
-    (20, 6, 0.05, "neel", "xy", 1),
-    (21, 6, 0.1, "vacuum", "circular_left", 0),
-    (21, 5, 0.0, "vacuum", "y", 0),
+@pytest.mark.parametrize("L,T,p,state,pol,toff,probe", [
+    (20, 7, 0.1, "vacuum", "x", 0, None),
+    (20, 6, 0.05, "neel", "xy", 1, None),
+    (21, 6, 0.1, "vacuum", "circular_left", 0, None),
+    (21, 5, 0.0, "vacuum", "y", 0, None),
+    (12, 6, 0.1, "vacuum", "x", 0, None),
+    (14, 7, 0.1, "neel", "y", 0, None),
+    (16, 6, 0.1, "vacuum", "x", 0, 5),
+    (18, 6, 0.1, "vacuum", "x", 1, 13),
+    (22, 8, 0.05, "vacuum", "y", 0, None),
 ])
-def test_echo_light_cone_end(pkg, engine, monkeypatch, L, T, p, state, pol, toff):
-    """Echo chains ending in the light-cone pass (the last two passes merged into
-    one measure-only pass over sites j-1..j+2 with the kicks outside the light
-    cone of Z_j dropped): the same per-trajectory echo as the oracle (1e-10) and
+def test_echo_light_cone_end(pkg, engine, monkeypatch, L, T, p, state, pol, toff, probe):
+    """Echo chains ending in the light-cone pass (the chain's last passes merged
+    into one measure-only pass over an 8-site window, each kick layer cut to the
+    light cone of Z_j): the same per-trajectory echo as the oracle (1e-10) and
     as the engine without the merge (DTC_NO_LIGHTCONE=1)."""
     rng = np.random.default_rng(L * 31 + T)
     hs, phis = random_disorder(rng, L, 2)
+    kw = {} if probe is None else {"probe_site": probe}
     spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
-                         initial_state=state, t_offset=toff)
+                         initial_state=state, t_offset=toff, **kw)
     got = engine.autocorr(spec, 3, seed=77)
     ref = c_oracle.autocorr(spec, 3, seed=77)
     _cmp(got, ref)
