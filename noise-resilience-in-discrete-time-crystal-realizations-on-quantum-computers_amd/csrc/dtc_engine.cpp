@@ -76,6 +76,7 @@ struct dtc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
+  DevBuf lc_diag;  // cone diagonals of the light-cone pass, [n_inst][kLcTab]
   DevBuf recs, recs1, pk;               // kick records (batch schedule / single pass), pass list
   DevBuf dev_thr, dev_jump, dev_kraus;  // device-like noise tables (dtc_autocorr_device)
   std::vector<dtc::PassKick> pk_host;   // staged pass list (alive until the stream syncs)
@@ -537,6 +538,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.no_store = no_store;
   A.lc_layers = ps.lc_layers;
   A.lc_mask = ps.lc_mask;
+  A.lc_diag = (const double2*)ctx->lc_diag.p;
   A.batch = batch;
   A.n_obs = n_obs;
   const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
@@ -712,12 +714,40 @@ uint64_t init_state_mask(const RunCfg& rc, uint64_t traj) {
   return m;
 }
 
+// Cone diagonals of the light-cone pass (dtc_kernels.h, kLcTab): for r = 1..4
+// the terms of D on sites j-r+1 .. j+r-1 and every bond touching them, as a
+// function of bits lo..hi = j-r .. j+r (clipped to [0, L)).
+void build_cone_tables(int L, int j, int n_inst, const double* h, const double* phi,
+                       std::vector<double>& out) {
+  out.assign((size_t)n_inst * dtc::kLcTab * 2, 0.0);
+  for (int in = 0; in < n_inst; ++in) {
+    const double* hh = h + (size_t)in * L;
+    const double* pp = phi + (size_t)in * (L > 1 ? L - 1 : 0);
+    for (int r = 1; r <= 4; ++r) {
+      const int lo = std::max(0, j - r), hi = std::min(L - 1, j + r);
+      double* o = out.data() + ((size_t)in * dtc::kLcTab + dtc::lc_tab_off(r)) * 2;
+      for (int v = 0; v < (1 << (hi - lo + 1)); ++v) {
+        const double ang = diag_angle(L, hh, pp, std::max(0, j - r + 1), j + r, j - r, j + r, lo, v);
+        o[2 * v] = std::cos(-0.5 * ang);
+        o[2 * v + 1] = std::sin(-0.5 * ang);
+      }
+    }
+  }
+}
+
 int upload_tables(dtc_ctx* ctx, const dtc_problem* pr, const Plan& pl) {
   std::vector<double> dt;
   build_diag_tables(pl, pr->n_inst, pr->h, pr->phi, dt);
   DTC_TRY(ensure(ctx->diag, dt.size() * sizeof(double)));
   DTC_HIP(hipMemcpyAsync(ctx->diag.p, dt.data(), dt.size() * sizeof(double),
                          hipMemcpyHostToDevice, ctx->stream));
+  if (pr->probe_site >= 0 && pr->probe_site < pr->L) {
+    std::vector<double> ct;
+    build_cone_tables(pr->L, pr->probe_site, pr->n_inst, pr->h, pr->phi, ct);
+    DTC_TRY(ensure(ctx->lc_diag, ct.size() * sizeof(double)));
+    DTC_HIP(hipMemcpyAsync(ctx->lc_diag.p, ct.data(), ct.size() * sizeof(double),
+                           hipMemcpyHostToDevice, ctx->stream));
+  }
   const int n_periods = std::max(1, pr->T - 1 + pr->t_offset);
   const size_t kb = (size_t)n_periods * pr->L * pr->n_sub * 8 * sizeof(double);
   DTC_TRY(ensure(ctx->kick, kb));
@@ -926,6 +956,7 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->vals_f);
   release(ctx->vals_e);
   release(ctx->diag);
+  release(ctx->lc_diag);
   release(ctx->kick);
   release(ctx->basis);
   release(ctx->sitemap);

@@ -57,10 +57,23 @@ enum PassShape { kShapeK = 0, kShapeKD = 1, kShapeDK = 2, kShapeKDK = 3, kShapeD
                  kShapeLC = 5 };
 static constexpr int kLcLayers = 5;
 static constexpr int kLcSites = 8;
-// LC records (compact, in the state's KickRec block read as doubles): layer l,
-// window site b -> doubles 2 (8 l + b) (coefficient) and + 1 (variant, as
-// integer); the global factor at doubles kLcTotal, kLcTotal + 1.
-static constexpr int kLcTotal = 2 * kLcLayers * kLcSites;
+// LC records (in the state's KickRec block read as doubles), Pauli frame form:
+// every kick i^k w Z^a X^b A(f) is applied as A(f^) (A = I + i f X for the RX
+// family, I + f ZX for RY), its Paulis carried to the probe: they flip the
+// sign of later coefficients on the site (f^), XOR the index of later
+// diagonals (x -> x ^ m) and the sign of Z_j.  Doubles [0, kLcCoefs): f^ of
+// (layer l, window site b) at 8 l + b (0: identity); kLcG2: prod w^2;
+// kLcPacked (as integer): bits 8 l .. 8 l + 7 = the frame's X mask after layer
+// l (window sites), bits 32..39 = the final one.
+static constexpr int kLcCoefs = kLcLayers * kLcSites;
+static constexpr int kLcG2 = kLcCoefs;
+static constexpr int kLcPacked = kLcCoefs + 1;
+// Cone diagonals: the D after layer l of M only matters through its terms on
+// sites j-r+1 .. j+r-1 (r = M - 1 - l; the terms elsewhere commute with
+// everything after it), a function of bits j-r .. j+r (clipped to [0, L)):
+// per instance one table per r = 1 .. 4 at offset (2^(2r+1) - 8) / 3.
+static constexpr int kLcTab = 680;
+__host__ __device__ constexpr int lc_tab_off(int r) { return ((1 << (2 * r + 1)) - 8) / 3; }
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
@@ -110,7 +123,7 @@ struct PassKick {
   int c, s, act;        // tile geometry (see PassArgs)
   int lc_layers;        // kShapeLC: layers lc[0 .. lc_layers), site b of layer l kicked
   KickDesc lc[kLcLayers];  // when bit 8 l + b of lc_mask is set (window site b = tile
-  uint64_t lc_mask;     // bit 4 + b); compact records (kLcTotal)
+  uint64_t lc_mask;     // bit 4 + b); Pauli-frame records (kLcCoefs ..)
 };
 
 struct PrepArgs {
@@ -174,6 +187,7 @@ struct PassArgs {
   int no_store;            // measure only: the tile is not written back (dst unused)
   int lc_layers;           // kShapeLC: kick layers; lc_mask bit 8 l + b = site b of layer l
   uint64_t lc_mask;
+  const double2* lc_diag;  // kShapeLC: cone diagonals, [n_inst][kLcTab]
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]

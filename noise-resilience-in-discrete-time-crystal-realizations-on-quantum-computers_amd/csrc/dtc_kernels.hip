@@ -24,6 +24,7 @@
 // GEMM-shaped).  Kicks of the RX family (every Pauli x RX(theta) has one real
 // and one imaginary entry per row) run as 4-flop-per-amplitude butterflies;
 // other kicks (RY products, circular polarization) use the general form.
+#include <cstdlib>
 #include <type_traits>
 
 #include "dtc_kernels.h"
@@ -254,29 +255,41 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   const uint64_t traj = (uint64_t)(P.traj_offset + (gstate % P.n_traj));
   KickRec* out = P.out + id * kRecPerState;
   if (pk.lc_layers > 0) {
-    // light-cone pass: compact records of the masked (layer, window site) kicks
+    // light-cone pass: Pauli-frame records (dtc_kernels.h, kLcCoefs ..)
     double* od = (double*)out;
     long long* oi = (long long*)out;
-    int ks = 0;
-    double wl = 1.0;
-    for (int l = 0; l < pk.lc_layers; ++l)
+    int fz = 0, fx = 0;  // the frame's Z / X exponents per window site
+    double g2 = 1.0;
+    long long packed = 0;
+    for (int l = 0; l < pk.lc_layers; ++l) {
       for (int b = 0; b < kLcSites; ++b) {
-        if (!((pk.lc_mask >> (kLcSites * l + b)) & 1ull)) continue;
-        const int lsite = pk.s + b;  // tile bit 4 + b >= c = 4
-        double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0),
-                        make_double2(1.0, 0.0)};
-        if (lsite < P.L_real)
-          build_site_kick(P, pk.lc[l], P.site_of ? P.site_of[lsite] : lsite, traj, m);
-        SiteMat sm;
-        canonicalise(pk.kind, m, sm);
-        od[2 * (kLcSites * l + b)] = sm.coef;
-        oi[2 * (kLcSites * l + b) + 1] = sm.var;
-        ks += sm.k;
-        wl *= sm.scale;
+        double fh = 0.0;
+        if ((pk.lc_mask >> (kLcSites * l + b)) & 1ull) {
+          const int lsite = pk.s + b;  // tile bit 4 + b >= c = 4
+          double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0),
+                          make_double2(0.0, 0.0), make_double2(1.0, 0.0)};
+          if (lsite < P.L_real)
+            build_site_kick(P, pk.lc[l], P.site_of ? P.site_of[lsite] : lsite, traj, m);
+          SiteMat sm;
+          canonicalise(pk.kind, m, sm);
+          // form A: i^k w Z^s A(beta); form B: S_B(alpha) = i X A(-alpha) (RX),
+          // R_B(alpha) = Z X R_A(-alpha) (RY)
+          const int form_b = sm.var >> 1, neg = sm.var & 1;
+          const double ft = form_b ? -sm.coef : sm.coef;
+          // the frame so far, moved past A(ft): Z flips f (RX); Z or X, not both (RY)
+          const int flip = ((pk.kind == kKindRX ? fz : (fz ^ fx)) >> b) & 1;
+          fh = flip ? -ft : ft;
+          fz ^= (pk.kind == kKindRX ? neg : (neg ^ form_b)) << b;
+          fx ^= form_b << b;
+          g2 *= sm.scale * sm.scale;
+        }
+        od[kLcSites * l + b] = fh;
       }
-    const int kph = ks & 3;
-    od[kLcTotal] = kph == 0 ? wl : (kph == 2 ? -wl : 0.0);
-    od[kLcTotal + 1] = kph == 1 ? wl : (kph == 3 ? -wl : 0.0);
+      if (l < 4) packed |= (long long)(fx & 0xFF) << (8 * l);
+    }
+    packed |= (long long)(fx & 0xFF) << 32;
+    od[kLcG2] = g2;
+    oi[kLcPacked] = packed;
     return;
   }
   int ksum = 0;
@@ -1161,35 +1174,41 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
   pass_body<kShapeD, NIBS, kKindRX, MC>(A);
 }
 
+static constexpr int kLcTilesPerGroup = 2;
+
 // ---- the light-cone end of an echo chain (kShapeLC) ------------------------
 // The chain ends with <Z_j>.  Going backward from the measurement, the last
 // kick layer matters only on j, the one before on j-1..j+1, the r-th from the
-// end on j-r..j+r (kicks are unitary and D is diagonal), so the chain's last
-// few passes collapse into one measure-only pass over tiles that hold the
-// window w0..w0+7 (tile bits 4..11; bits 0..3 = sites 0..3 as columns, c = 4):
-// layer l = 0 .. lc_layers-1 kicks the window sites its mask keeps -- nibble 2
-// then 1 for even l, 1 then 2 for odd l, one LDS re-layout between them --
-// with D (conjugated: echo) between consecutive layers; then the probe.
-// Compact records (kLcTotal): (layer, site) -> coefficient, variant.
-template <int KIND>
+// end on j-r..j+r (kicks are unitary and D is diagonal with nearest-neighbour
+// terms), so the chain's last few passes collapse into one measure-only pass
+// over tiles that hold the window w0..w0+7 (tile bits 4..11; bits 0..3 =
+// sites 0..3 as columns, c = 4): layer l = 0 .. lc_layers-1 kicks the window
+// sites its mask keeps -- nibble 2 then 1 for even l, 1 then 2 for odd l, one
+// LDS re-layout between them -- with the cone diagonal (conjugated: echo)
+// between consecutive layers; then the probe.  Kicks in Pauli-frame form
+// (dtc_kernels.h): one butterfly variant, no branches per site; a nibble of a
+// layer runs when any of its sites is kicked (identity f = 0 for the others).
+// A workgroup takes TPB consecutive tiles of one state: the records and tables
+// are staged once, and the next tile's 16 loads are issued before the current
+// tile's layers (register double buffer: the pass is VALU/LDS-heavy per byte).
+template <int KIND, int TPB>
 __device__ __forceinline__ void lc_body(const PassArgs& A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
   __shared__ double2 s_tile[kTile];
-  __shared__ double2 s_chunk[kMaxChunks * 64];
-  __shared__ double2 s_win[2][64];
+  __shared__ double2 s_cone[kLcTab];
   __shared__ double s_red[kThreads / 64][2];
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;  // c = 4, s = w0
   const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
   const int64_t b = blockIdx.y;
-  const int64_t tile = blockIdx.x;
+  const int64_t tile0 = (int64_t)blockIdx.x * TPB;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   RecRegs R;
   {
     const int lane = t & 63;
     const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
     double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcTotal + 2) {  // the compact records: lanes 0 .. 20
+    if (4 * lane < kLcPacked + 1) {  // the records: lanes 0 .. 10
       r0 = rp[0];
       r1 = rp[1];
     }
@@ -1200,144 +1219,159 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
   M.c = c;
   M.s = s;
   M.cmask = (1 << c) - 1;
-  M.tbase = ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
-  // diagonal tables: chunks + the window tables of layouts 1 (g0 = s) and 2 (s + 4)
-  constexpr int kChunkPerThread = (kMaxChunks * 64 + kThreads - 1) / kThreads;
-  double2 dchunk[kChunkPerThread];
-  double2 dwin = make_double2(1.0, 0.0);
-  const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
+  auto tbase_of = [&](int64_t tile) {
+    return ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
+  };
+  M.tbase = tbase_of(tile0);
+  constexpr int kConePerThread = (kLcTab + kThreads - 1) / kThreads;
+  double2 cv[kConePerThread];
+  const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
 #pragma unroll
-  for (int j = 0; j < kChunkPerThread; ++j) {
+  for (int j = 0; j < kConePerThread; ++j) {
     const int i = t + j * kThreads;
-    if (i < A.n_chunks * 64) dchunk[j] = dt[i];
+    if (i < kLcTab) cv[j] = ct[i];
   }
-  if (t < 128) dwin = dt[(A.n_chunks + s + 4 * (t >> 6)) * 64 + (t & 63)];
   // the tile in layout 2 (threads = tile bits 0..7: 16-amplitude runs)
   const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
-  double2 v[kRegs];
-  {
-    const char* src = (const char*)(A.src + b * A.state_len);
+  const char* src = (const char*)(A.src + b * A.state_len);
+  auto load_tile = [&](double2 (&dst)[kRegs], int64_t tb) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      const char* a = src + ((M.tbase | M.rel(r << 8)) << 4) + vofs;
+      const char* a = src + ((tb | M.rel(r << 8)) << 4) + vofs;
       const d2v w = __builtin_nontemporal_load((const d2v*)a);
-      v[r] = make_double2(w.x, w.y);
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0x4F70);  // tables landed, the tile's 16 loads in flight
-  const double cs = A.diag_conj ? -1.0 : 1.0;
-#pragma unroll
-  for (int j = 0; j < kChunkPerThread; ++j) {
-    const int i = t + j * kThreads;
-    if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
-  }
-  if (t < 128) s_win[t >> 6][t & 63] = make_double2(dwin.x, cs * dwin.y);
-  // (visible after the first re-layout's barrier)
-  // record (layer l, window site q) in the compact layout
-  auto coef = [&](int l, int q) { return R.d(0, 2 * (kLcSites * l + q)); };
-  auto var = [&](int l, int q) { return R.i(0, 2 * (kLcSites * l + q) + 1); };
-  // the kicks' global factor (a phase times the product of the real scales):
-  // only its modulus matters to the probe
-  const double g2 = fma(R.d(0, kLcTotal), R.d(0, kLcTotal), R.d(0, kLcTotal + 1) * R.d(0, kLcTotal + 1));
-
-  auto kick = [&](auto n_tag, auto l_tag) {
-    constexpr int N = decltype(n_tag)::value;  // nibble = layout in registers
-    constexpr int l = decltype(l_tag)::value;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int site = 4 * (N - 1) + q;  // window site of tile bit 4 N + q
-      if (!((A.lc_mask >> (kLcSites * l + site)) & 1ull)) continue;
-      const double f = coef(l, site);
-      const int vv = var(l, site);
-      auto run = [&](auto qtag) {
-        constexpr int Q = decltype(qtag)::value;
-        if (vv == 0) layer_f<KIND, 0, Q>(v, f);
-        else if (vv == 1) layer_f<KIND, 1, Q>(v, f);
-        else if (vv == 2) layer_f<KIND, 2, Q>(v, f);
-        else layer_f<KIND, 3, Q>(v, f);
-      };
-      if (q == 0) run(std::integral_constant<int, 0>{});
-      else if (q == 1) run(std::integral_constant<int, 1>{});
-      else if (q == 2) run(std::integral_constant<int, 2>{});
-      else run(std::integral_constant<int, 3>{});
+      dst[r] = make_double2(w.x, w.y);
     }
   };
-  auto diag = [&](auto lay_tag) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int g0 = s + 4 * LAY - c;  // the window of the nibble in registers
-    const double2* win = s_win[LAY - 1];
-    const int64_t x0 = M.at(ybase<LAY>(t));
-    const int w0i = (int)(((x0 << 1) >> g0) & 63);
-    const double2 w0 = win[w0i];
-    const double2 pc = cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y));
+  double2 v[kRegs];
+  load_tile(v, M.tbase);
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // records and tables landed, the tile's 16 loads in flight
+  const double cs = A.diag_conj ? -1.0 : 1.0;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, win[w0i | (r << 1)]));
+  for (int j = 0; j < kConePerThread; ++j) {
+    const int i = t + j * kThreads;
+    if (i < kLcTab) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
+  }
+  // (visible after the first re-layout's barrier)
+  const double g2 = R.d(0, kLcG2);
+  const long long packed = R.bits(kLcPacked);
+  const int nl = A.lc_layers;
+  const int jp = A.probe;
+
+  // kicks of nibble N (window sites 4 (N-1) .. 4 (N-1) + 3) in layer l
+  auto kick = [&](double2 (&v)[kRegs], auto n_tag, auto l_tag) {
+    constexpr int N = decltype(n_tag)::value;
+    constexpr int l = decltype(l_tag)::value;
+    constexpr int k0 = kLcSites * l + 4 * (N - 1);
+    if (!((A.lc_mask >> k0) & 0xFull)) return;
+    layer_f<KIND, 0, 0>(v, R.d(0, k0));
+    layer_f<KIND, 0, 1>(v, R.d(0, k0 + 1));
+    layer_f<KIND, 0, 2>(v, R.d(0, k0 + 2));
+    layer_f<KIND, 0, 3>(v, R.d(0, k0 + 3));
+  };
+  // cone diagonal after layer l, applied in layout LAY: D_r(x ^ m_l), one
+  // table lookup and one complex product per amplitude
+  auto diag = [&](double2 (&v)[kRegs], auto lay_tag, int l) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int rad = nl - 1 - l;
+    const int lo = max(0, jp - rad), hi = min(A.L_real - 1, jp + rad);
+    const int msk = (1 << (hi - lo + 1)) - 1;
+    const int g0 = s + 4 * LAY - c;  // global bit of register bit 0
+    const int64_t m = (int64_t)((packed >> (8 * l)) & 0xFF) << s;
+    const int base = (int)(((M.at(ybase<LAY>(t)) ^ m) >> lo) & msk);
+    const double2* tab = s_cone + lc_tab_off(rad);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const int off = (g0 >= lo ? (r << (g0 - lo)) : (r >> (lo - g0))) & msk;
+      v[r] = cmul(v[r], tab[base ^ off]);
+    }
   };
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
-  const int nl = A.lc_layers;
-  // layer 0: nibble 2 (layout 2), re-layout, nibble 1 (layout 1), D
-  kick(L2{}, std::integral_constant<int, 0>{});
-  exchange<2, 1>(v, s_tile, t);
-  kick(L1{}, std::integral_constant<int, 0>{});
-  if (nl > 1) diag(L1{});
-  if (nl > 1) {  // layer 1: 1 -> 2
-    kick(L1{}, std::integral_constant<int, 1>{});
-    exchange<1, 2>(v, s_tile, t);
-    kick(L2{}, std::integral_constant<int, 1>{});
-    if (nl > 2) diag(L2{});
-  }
-  if (nl > 2) {  // layer 2: 2 -> 1
-    kick(L2{}, std::integral_constant<int, 2>{});
+  // one tile, its amplitudes in v (layout 2)
+  auto process = [&](double2 (&v)[kRegs], int64_t tile) {
+    M.tbase = tbase_of(tile);
+    // layer 0: nibble 2 (layout 2), re-layout, nibble 1 (layout 1), D
+    kick(v, L2{}, std::integral_constant<int, 0>{});
     exchange<2, 1>(v, s_tile, t);
-    kick(L1{}, std::integral_constant<int, 2>{});
-    if (nl > 3) diag(L1{});
-  }
-  if (nl > 3) {  // layer 3: 1 -> 2
-    kick(L1{}, std::integral_constant<int, 3>{});
-    exchange<1, 2>(v, s_tile, t);
-    kick(L2{}, std::integral_constant<int, 3>{});
-    if (nl > 4) diag(L2{});
-  }
-  if (nl > 4) {  // layer 4: 2 -> 1
-    kick(L2{}, std::integral_constant<int, 4>{});
-    exchange<2, 1>(v, s_tile, t);
-    kick(L1{}, std::integral_constant<int, 4>{});
-  }
-  // probe: layout 1 after an odd number of layers, 2 after an even number
-  const int lay = (nl & 1) ? 1 : 2;
-  double ptot = 0.0, pz = 0.0;
-  {
-    const int64_t x0 = lay == 1 ? M.at(ybase<1>(t)) : M.at(ybase<2>(t));
-    const int site = A.probe;
-    const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
-    const int jr = tb - 4 * lay;  // register bit of the probe, if in the nibble in registers
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
-      ptot += p2;
-      pz += (jr >= 0 && jr < 4 && ((r >> jr) & 1)) ? -p2 : p2;
+    kick(v, L1{}, std::integral_constant<int, 0>{});
+    if (nl > 1) {  // layer 1: 1 -> 2
+      diag(v, L1{}, 0);
+      kick(v, L1{}, std::integral_constant<int, 1>{});
+      exchange<1, 2>(v, s_tile, t);
+      kick(v, L2{}, std::integral_constant<int, 1>{});
     }
-    if (!(jr >= 0 && jr < 4)) pz = ((x0 >> site) & 1) ? -ptot : ptot;
-  }
-  const int wave = t >> 6, lane = t & 63;
-  const double tot = wave_sum(ptot) * g2;
-  const double z = wave_sum(pz) * g2;
-  if (lane == 0) {
-    s_red[wave][0] = tot;
-    s_red[wave][1] = z;
-  }
-  __syncthreads();
-  if (t < 2) {
-    double acc = 0.0;
-    for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][t];
-    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    if (nl > 2) {  // layer 2: 2 -> 1
+      diag(v, L2{}, 1);
+      kick(v, L2{}, std::integral_constant<int, 2>{});
+      exchange<2, 1>(v, s_tile, t);
+      kick(v, L1{}, std::integral_constant<int, 2>{});
+    }
+    if (nl > 3) {  // layer 3: 1 -> 2
+      diag(v, L1{}, 2);
+      kick(v, L1{}, std::integral_constant<int, 3>{});
+      exchange<1, 2>(v, s_tile, t);
+      kick(v, L2{}, std::integral_constant<int, 3>{});
+    }
+    if (nl > 4) {  // layer 4: 2 -> 1
+      diag(v, L2{}, 3);
+      kick(v, L2{}, std::integral_constant<int, 4>{});
+      exchange<2, 1>(v, s_tile, t);
+      kick(v, L1{}, std::integral_constant<int, 4>{});
+    }
+    // probe: layout 1 after an odd number of layers, 2 after an even number;
+    // the frame's X on j flips it
+    const int lay = (nl & 1) ? 1 : 2;
+    double ptot = 0.0, pz = 0.0;
+    {
+      const int64_t x0 = lay == 1 ? M.at(ybase<1>(t)) : M.at(ybase<2>(t));
+      const int tb = jp < c ? jp : ((jp >= s && jp < s + kTileBits - c) ? c + jp - s : -1);
+      const int jr = tb - 4 * lay;  // register bit of the probe, if in the nibble in registers
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+        ptot += p2;
+        pz += (jr >= 0 && jr < 4 && ((r >> jr) & 1)) ? -p2 : p2;
+      }
+      if (!(jr >= 0 && jr < 4)) pz = ((x0 >> jp) & 1) ? -ptot : ptot;
+      if ((packed >> (32 + jp - s)) & 1) pz = -pz;
+    }
+    const int wave = t >> 6, lane = t & 63;
+    const double tot = wave_sum(ptot) * g2;
+    const double z = wave_sum(pz) * g2;
+    if (lane == 0) {
+      s_red[wave][0] = tot;
+      s_red[wave][1] = z;
+    }
+    __syncthreads();
+    if (t < 2) {
+      double acc = 0.0;
+      for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
+      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    }
+  };
+  // two register buffers, no copies: the loads of tile i+1 fly while tile i runs
+  static_assert(TPB == 1 || TPB == 2 || TPB == 4, "tiles per workgroup");
+  if constexpr (TPB == 1) {
+    process(v, tile0);
+  } else {
+    double2 w[kRegs];
+    load_tile(w, tbase_of(tile0 + 1));
+    process(v, tile0);
+    if constexpr (TPB == 4) {
+      load_tile(v, tbase_of(tile0 + 2));
+      process(w, tile0 + 1);
+      load_tile(w, tbase_of(tile0 + 3));
+      process(v, tile0 + 2);
+      process(w, tile0 + 3);
+    } else {
+      process(w, tile0 + 1);
+    }
   }
 }
 
-template <int KIND>
+template <int KIND, int TPB>
 __global__ __launch_bounds__(kThreads, 2) void dtc_lc_final(PassArgs A) {
-  lc_body<KIND>(A);
+  lc_body<KIND, TPB>(A);
 }
 
 template <int NIBS, int KIND, int MC>
@@ -1415,14 +1449,22 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
   if (shape == kShapeLC) {
     // measure-only light-cone pass: probe, window at tile bits 4..11 (c = 4)
     if (a.c != 4 || a.act != 0xFF0 || a.meas != kMeasProbe || !a.no_store || a.lc_layers < 1 ||
-        a.lc_layers > kLcLayers || a.n_obs < 2)
+        a.lc_layers > kLcLayers || a.n_obs < 2 || !a.lc_diag)
       return hipErrorInvalidValue;
-    if (kind == kKindRX)
-      hipLaunchKernelGGL((dtc_lc_final<kKindRX>), grid, dim3(kThreads), 0, stream, a);
-    else if (kind == kKindRY)
-      hipLaunchKernelGGL((dtc_lc_final<kKindRY>), grid, dim3(kThreads), 0, stream, a);
+    // several tiles per workgroup (register double buffer) when they divide the state
+    int tpb = kLcTilesPerGroup;
+    if (const char* e = std::getenv("DTC_LC_TPB")) tpb = std::atoi(e);  // development A/B
+    while (tpb > 1 && n_tiles % tpb) tpb >>= 1;
+    if (tpb != 1 && tpb != 2 && tpb != 4) tpb = 1;
+    grid.x = n_tiles / tpb;
+    if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
+    const bool rx = kind == kKindRX;
+    if (tpb == 4)
+      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 4> : dtc_lc_final<kKindRY, 4>), grid, dim3(kThreads), 0, stream, a);
+    else if (tpb == 2)
+      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 2> : dtc_lc_final<kKindRY, 2>), grid, dim3(kThreads), 0, stream, a);
     else
-      return hipErrorInvalidValue;
+      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 1> : dtc_lc_final<kKindRY, 1>), grid, dim3(kThreads), 0, stream, a);
     return hipGetLastError();
   }
   int nibs = 0;
