@@ -1607,10 +1607,29 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
     DTC_HIP(hipMemsetAsync(vals, 0, (size_t)nb * T * n_v * sizeof(double), ctx->stream));
     const int64_t vs = (int64_t)T * n_v;
-    for (const EPass& e : sched) {
+    // kick records of the schedule's passes: one prep launch per segment
+    // (the X-basis passes of the device path build their own)
+    const size_t per_pass = (size_t)nb * dtc::kRecPerState * sizeof(dtc::KickRec);
+    const size_t seg = std::max<size_t>(1, std::min<size_t>(sched.size(), (size_t)(256u << 20) / per_pass));
+    DTC_TRY(ensure(ctx->recs, seg * per_pass));
+    ctx->pk_host.resize(sched.size());
+    for (size_t i = 0; i < sched.size(); ++i) ctx->pk_host[i] = pass_kick(rc, sched[i].ps);
+    DTC_TRY(ensure(ctx->pk, sched.size() * sizeof(dtc::PassKick)));
+    DTC_HIP(hipMemcpyAsync(ctx->pk.p, ctx->pk_host.data(), sched.size() * sizeof(dtc::PassKick),
+                           hipMemcpyHostToDevice, ctx->stream));
+    for (size_t i = 0; i < sched.size(); ++i) {
+      const EPass& e = sched[i];
+      if (i % seg == 0) {
+        dtc::PrepArgs Pp = prep_args(ctx, rc, bs, nb);
+        Pp.passes = (const dtc::PassKick*)ctx->pk.p + i;
+        Pp.n_pass = (int)std::min(seg, sched.size() - i);
+        Pp.out = (dtc::KickRec*)ctx->recs.p;
+        DTC_HIP(dtc::launch_prep(Pp, ctx->stream));
+      }
+      const dtc::KickRec* recs = (const dtc::KickRec*)ctx->recs.p + (i % seg) * nb * dtc::kRecPerState;
       DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, e.ps, F, F,
                                e.parts ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_obs, nullptr,
-                               0, nullptr, e.parts));
+                               0, recs, e.parts));
       if (e.parts & dtc::kPartZ)
         DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb, vals + (size_t)e.t_mid * n_v, vs,
                                    0, (e.parts & dtc::kPartXPost) ? 3 * L : 2 * L, 1));

@@ -1483,34 +1483,37 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
 // out[b][o] = sum over tiles of partial[b][tile][o]: one workgroup per
 // (state, 8 observables), fixed summation order (strided per thread, then an
 // LDS tree), so results do not depend on the batch a state ran in.
+// Per-state sums over tiles: a workgroup per (state, block of up to 256
+// columns); thread t sums column t % cols over every (256 / cols)-th tile,
+// coalesced across the columns, then the column's groups are added in LDS
+// (fixed order: results do not depend on the batch).
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partial,
                                                      int n_tiles, int n_obs, int o_first,
-                                                     int n_out, int accumulate,
+                                                     int n_out, int cols, int accumulate,
                                                      double* __restrict__ out,
                                                      int64_t out_stride) {
-  __shared__ double s_acc[8][256];
-  const int b = blockIdx.y, o0 = blockIdx.x * 8, t = threadIdx.x;
-  const int no = min(8, n_out - o0);
-  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int k = t; k < n_tiles; k += 256) {
-    const double* p = partial + ((int64_t)b * n_tiles + k) * n_obs + o_first + o0;
+  __shared__ double s_acc[256];
+  const int b = blockIdx.y, t = threadIdx.x;
+  const int o = blockIdx.x * cols + t % cols, grp = t / cols, ngrp = 256 / cols;
+  double acc = 0.0;
+  if (o < n_out) {
+    const double* p = partial + (int64_t)b * n_tiles * n_obs + o_first + o;
+    double a2[4] = {0.0, 0.0, 0.0, 0.0};
+    int k = grp;
+    for (; k + 3 * ngrp < n_tiles; k += 4 * ngrp) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < no) acc[j] += p[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s_acc[j][t] = acc[j];
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_acc[j][t] += s_acc[j][t + w];
+      for (int u = 0; u < 4; ++u) a2[u] += p[(int64_t)(k + u * ngrp) * n_obs];
     }
-    __syncthreads();
+    for (; k < n_tiles; k += ngrp) a2[0] += p[(int64_t)k * n_obs];
+    acc = (a2[0] + a2[1]) + (a2[2] + a2[3]);
   }
-  if (t < no) {
-    double* o = out + (int64_t)b * out_stride + o0 + t;
-    *o = accumulate ? *o + s_acc[t][0] : s_acc[t][0];
+  s_acc[t] = acc;
+  __syncthreads();
+  if (grp == 0 && o < n_out) {
+    double sum = s_acc[t];
+    for (int g = 1; g < ngrp; ++g) sum += s_acc[g * cols + t];
+    double* dst = out + (int64_t)b * out_stride + o;
+    *dst = accumulate ? *dst + sum : sum;
   }
 }
 
@@ -1519,8 +1522,9 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
                          int n_out, int accumulate) {
   if (n_out < 0) n_out = n_obs - o_first;
   if (o_first < 0 || n_out < 1 || o_first + n_out > n_obs) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reduce_kernel, dim3((n_out + 7) / 8, batch), dim3(256), 0, stream, partial,
-                     n_tiles, n_obs, o_first, n_out, accumulate, out, out_stride);
+  const int cols = n_out <= 16 ? 16 : (n_out <= 32 ? 32 : (n_out <= 64 ? 64 : (n_out <= 128 ? 128 : 256)));
+  hipLaunchKernelGGL(reduce_kernel, dim3((n_out + cols - 1) / cols, batch), dim3(256), 0, stream,
+                     partial, n_tiles, n_obs, o_first, n_out, cols, accumulate, out, out_stride);
   return hipGetLastError();
 }
 
