@@ -164,6 +164,67 @@ def spawn_ranks(n: int, argv) -> int:
     return rc
 
 
+def _child_env(port: int, rank: int, local_rank: int, world: int) -> dict:
+    """Environment of a rank of a nested job: its own rendezvous on 127.0.0.1.
+    torchrun's agent variables are dropped (TORCHELASTIC_USE_AGENT_STORE would
+    make the child connect to the agent's store instead of hosting its own)."""
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("TORCHELASTIC_", "TORCH_ELASTIC_"))}
+    env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
+                "RANK": str(rank), "LOCAL_RANK": str(local_rank),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "ROLE_RANK": str(rank)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def run_child_ranks(child_argv, dist, rank: int, local_rank: int, world: int,
+                    timeout_s: float, coll_dev: str = "cpu"):
+    """Run a second N-rank job of this script from inside a running one: every
+    rank starts one child (a subprocess, never an exec), the children
+    rendezvous on a port rank 0 picked and broadcast over ``dist``, and the
+    parents wait for them at most ``timeout_s`` (a child still running then is
+    killed with its process group).  A failure of the nested job can therefore
+    not hang or end the outer one.  Returns rank 0's parsed JSON line, or
+    {"error": ...}; other ranks return None."""
+    import signal
+    import subprocess
+
+    import torch
+
+    port = torch.tensor([_free_port() if rank == 0 else 0], dtype=torch.int64, device=coll_dev)
+    if dist:
+        dist.broadcast(port, 0)
+    env = _child_env(int(port.item()), rank, local_rank, world)
+    t0 = time.perf_counter()
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(child_argv), env=env,
+                         stdout=subprocess.PIPE if rank == 0 else subprocess.DEVNULL,
+                         text=True, start_new_session=True)
+    status = "ok"
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        status = f"timeout after {timeout_s:.0f} s"
+    ok = torch.tensor([1.0 if (status == "ok" and p.returncode == 0) else 0.0],
+                      dtype=torch.float64, device=coll_dev)
+    if dist:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if rank != 0:
+        return None
+    wall = time.perf_counter() - t0
+    if status != "ok" or p.returncode != 0 or float(ok.item()) < 1.0:
+        return {"error": status if status != "ok" else
+                f"a rank of the nested job failed (rank 0 exit code {p.returncode})",
+                "wall_s": wall}
+    lines = [ln for ln in (out or "").splitlines() if ln.strip().startswith("{")]
+    if not lines:
+        return {"error": "no JSON line from the nested job", "wall_s": wall}
+    d = json.loads(lines[-1])
+    d["wall_s"] = wall
+    return d
+
+
 def spawn_selftest(args) -> int:
     """Rank-side half of the spawn check (tests/test_bench_spawn.py): every
     rank joins a gloo group, the world size and the ranks are all-reduced,
@@ -181,12 +242,28 @@ def spawn_selftest(args) -> int:
     if world > 1:
         dist.all_reduce(t)
         dist.barrier()
+    nested = None
+    if args.selftest_nested and world > 1:
+        # the C5 sub-run's plumbing (run_child_ranks) with a selftest as the child
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        fail = os.environ.get("BENCH_SELFTEST_NESTED_HANG_RANK")
+        child = ["--gpus", str(world), "--spawn-selftest"]
+        env_hang = fail is not None and fail == str(rank)
+        if env_hang:
+            os.environ["BENCH_SELFTEST_HANG"] = "1"
+        nested = run_child_ranks(child, dist, rank, local_rank, world,
+                                 timeout_s=args.nested_timeout)
+        os.environ.pop("BENCH_SELFTEST_HANG", None)
+    if os.environ.get("BENCH_SELFTEST_HANG") == "1":
+        time.sleep(3600)  # test hook: a nested rank that never finishes
     if rank == 0:
         B = args.strong_total // world if args.strong_total else args.batch
-        print(json.dumps({"metric": "spawn-selftest", "value": float(t[0]), "n_gpus": world,
-                          "rank_sum": float(t[1]),
-                          "scaling": "strong" if args.strong_total else "weak",
-                          "trajectories_per_step_per_gpu": B}), flush=True)
+        d = {"metric": "spawn-selftest", "value": float(t[0]), "n_gpus": world,
+             "rank_sum": float(t[1]), "scaling": "strong" if args.strong_total else "weak",
+             "trajectories_per_step_per_gpu": B}
+        if nested is not None:
+            d["nested"] = nested
+        print(json.dumps(d), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -251,6 +328,14 @@ def main(argv=None):
                          "scaling with --batch per GPU")
     ap.add_argument("--spawn-selftest", action="store_true",
                     help="CPU-only check of the rank spawn path (gloo, no GPU work)")
+    ap.add_argument("--selftest-nested", action="store_true",
+                    help="with --spawn-selftest: also run a nested selftest job through "
+                         "run_child_ranks (the C5 sub-run's plumbing)")
+    ap.add_argument("--nested-timeout", type=float, default=300.0,
+                    help="seconds a nested job (the C5 sub-run) may take before it is killed")
+    ap.add_argument("--no-c5-subrun", action="store_true",
+                    help="c2 at 8 GPUs: skip the C5 (L=34 over 8 GPUs) sub-run that is "
+                         "attached to the line as \"c5\"")
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -373,11 +458,6 @@ def main(argv=None):
         dist.all_gather(per_rank, my)
     per_rank = [r.cpu().numpy() for r in per_rank]
 
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
-
     total_units = world * args.steps * B * per_traj
     value = total_units / elapsed
     lo = stats[0]
@@ -389,11 +469,24 @@ def main(argv=None):
     traffic, traffic_src = read_traffic(launch_bytes)
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and not c3:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
         threads = host_cpu_info()["usable_cores"]
         cpu = cpu_baseline(spec, args.cpu_traj or 4 * threads, args.cpu_tf, threads)
 
     info = eng.device_info()
+    c5 = None
+    if world == 8 and args.config == "c2" and not args.no_c5_subrun:
+        # SURVEY.md §8(d) C5 (one L=34 state over the 8 GPUs) as a nested 8-rank
+        # job after the timed C2 region, so the node's 8-GPU run also measures
+        # it; its failure or hang cannot touch the C2 line (run_child_ranks)
+        eng.close()
+        torch.cuda.empty_cache()
+        c5 = run_child_ranks(["--config", "c5", "--gpus", "8", "--steps", "1", "--warmup", "1"],
+                             dist, rank, local_rank, world, args.nested_timeout, cdev)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
     res = {
         "metric": METRIC if not c3 else METRIC.replace("at L=20", "at L=20 (C3 device-like noise)"),
         "value": value,
@@ -467,6 +560,8 @@ def main(argv=None):
     }
     if cpu:
         res["cpu_baseline"] = cpu
+    if c5 is not None:
+        res["c5"] = c5
     print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -33,6 +33,33 @@ def test_spawn_yields_n_ranks_one_json_line(n):
     assert d["trajectories_per_step_per_gpu"] == 1024 // n
 
 
+def test_nested_job_from_ranks():
+    """The plumbing of the 8-GPU line's C5 sub-run (bench.run_child_ranks):
+    every rank starts one child, the children form their own group on a port
+    rank 0 broadcast, and rank 0 attaches the nested job's JSON line."""
+    r = _run(["--gpus", "2", "--spawn-selftest", "--selftest-nested"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] == 2
+    assert d["nested"]["n_gpus"] == 2 and d["nested"]["value"] == 2
+    assert d["nested"]["rank_sum"] == 1
+
+
+def test_nested_job_hang_is_contained():
+    """A nested rank that never finishes is killed at the timeout; the outer
+    job still prints its line, with the nested job's error."""
+    r = _run(["--gpus", "2", "--spawn-selftest", "--selftest-nested", "--nested-timeout", "20"],
+             {"BENCH_SELFTEST_NESTED_HANG_RANK": "1"})
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 2
+    assert "error" in d["nested"]
+
+
 def test_world_size_mismatch_refused():
     r = _run(["--gpus", "8", "--spawn-selftest"], {"WORLD_SIZE": "2", "RANK": "0",
                                                    "LOCAL_RANK": "0"})
