@@ -475,13 +475,17 @@ def main(argv=None):
 
     info = eng.device_info()
     c5 = None
-    if world == 8 and args.config == "c2" and not args.no_c5_subrun:
+    force_c5 = os.environ.get("BENCH_C5_SUBRUN") == "1"  # plumbing check on a 1-GPU box
+    if (world == 8 or force_c5) and args.config == "c2" and not args.no_c5_subrun:
         # SURVEY.md §8(d) C5 (one L=34 state over the 8 GPUs) as a nested 8-rank
         # job after the timed C2 region, so the node's 8-GPU run also measures
-        # it; its failure or hang cannot touch the C2 line (run_child_ranks)
+        # it; its failure or hang cannot touch the C2 line (run_child_ranks).
+        # Forced at other rank counts it runs the same driver as --config c5
+        # there (1 GPU: 8 virtual shards of L=31)
         eng.close()
         torch.cuda.empty_cache()
-        c5 = run_child_ranks(["--config", "c5", "--gpus", "8", "--steps", "1", "--warmup", "1"],
+        c5 = run_child_ranks(["--config", "c5", "--gpus", str(world), "--steps", "1",
+                              "--warmup", "1"],
                              dist, rank, local_rank, world, args.nested_timeout, cdev)
     if rank != 0:
         if dist:
@@ -861,7 +865,7 @@ def main_energy(args):
     = `--batch` trajectories per GPU; <H(t)>/L of instance 0 is formed on the
     host from the trajectory means (energy.energy_from_observables).  Value =
     trajectories x (tf-1) periods per second over all ranks (each period also
-    measures Z, ZZ and X, the X basis by one extra kick pass per site group)."""
+    measures Z, ZZ and X, all in flight inside the period's pass)."""
     world, rank, local_rank, dist = _init_dist()
     pkg = importlib.import_module(PKG)
     L, T, B = args.L, args.tf, args.batch

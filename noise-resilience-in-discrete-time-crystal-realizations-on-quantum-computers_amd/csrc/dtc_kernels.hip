@@ -977,10 +977,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // <X> partials of the 4 sites in register nibble LAY (energy mode): lanes
   // 0, 16, 32, 48 of each wave end with the wave sums of register bits 0..3
   // (2 + 1 shuffles halve the 4 values over lane bits 5, 4; 4 more finish).
-  auto measure_x = [&](auto lay_tag, double scale, int slot0) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int wave = t >> 6, lane = t & 63;
-    double a[4];
+  auto pair_sums = [&](auto lay_tag, double (&a)[4], double scale) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       double x = 0.0;
@@ -990,10 +987,23 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         const double2 u = v[r], w = v[r | (1 << q)];
         x = fma(u.x, w.x, fma(u.y, w.y, x));
       }
-      a[q] = x;
+      a[q] = 2.0 * scale * x;
     }
+  };
+  auto measure_x = [&](auto lay_tag, double scale, int slot0) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int wave = t >> 6, lane = t & 63;
+    double a[4];
+    pair_sums(lay_tag, a, scale);
     const double k = wave_sum_multi<4>(a);
-    if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = 2.0 * scale * k;
+    if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = k;
+  };
+  // X before the post-kick: each thread's pair sums only; their wave
+  // reductions run after the tile's stores are issued (x_post_finish)
+  double xpost[3][4];
+  auto measure_x_post = [&](auto lay_tag, double scale) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    pair_sums(lay_tag, xpost[LAY], scale);
   };
   // squared share of the global factor carried by the factored kicks of
   // nibble N (records rec0 + 4N .. +3): measuring after them multiplies sums by
@@ -1056,19 +1066,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     double sc = inv_w2_mid;
     if constexpr (RP::nO) {
       exchange<RP::d_lay, RP::O>(v, s_tile, t);
-      if (x_post) measure_x(LO{}, sc, kSlotXPost);
+      if (x_post) measure_x_post(LO{}, sc);
       apply_nibble<RP::O, KIND>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(RP::O, kTileBits);
     }
     if constexpr (RP::n0) {
       exchange<RP::pO, 0>(v, s_tile, t);
-      if (x_post) measure_x(L0{}, sc, kSlotXPost);
+      if (x_post) measure_x_post(L0{}, sc);
       apply_nibble<0, KIND>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(0, kTileBits);
     }
     if constexpr (RP::nIO) {
       exchange<RP::p0, RP::IO>(v, s_tile, t);
-      if (x_post) measure_x(LIO{}, sc, kSlotXPost);
+      if (x_post) measure_x_post(LIO{}, sc);
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
     exchange<RP::pIO, RP::IO>(v, s_tile, t);
@@ -1111,6 +1121,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   if constexpr (MC >= 2) {
     // measurement combines after the tile's stores are issued (one barrier)
+    if constexpr (MC == 3 && RP::post) {
+      if (x_post) {
+        const int wave = t >> 6, lane = t & 63;
+        auto finish = [&](auto lay_tag) {
+          constexpr int LAY = decltype(lay_tag)::value;
+          const double k = wave_sum_multi<4>(xpost[LAY]);
+          if ((lane & 15) == 0) s_red[wave][kSlotXPost + 4 * LAY + (lane >> 4)] = k;
+        };
+        if constexpr (RP::nO) finish(LO{});
+        if constexpr (RP::n0) finish(L0{});
+        if constexpr (RP::nIO) finish(LIO{});
+      }
+    }
     if (zc_lay >= 0 || x_pre || x_post) {
       __syncthreads();
       if (zc_lay >= 0) site_combine(zc_lay, zc_inv);

@@ -23,6 +23,13 @@ def _cmp(a, b, tol=TOL):
 
 CASES = [
     # L, T, n_inst, n_traj, p, state, pol, t_offset
+    # edge sizes: one- to three-site chains (sites 1..11 of the 12-bit tile are
+    # padding) and the shortest sweeps (T=1: only t=0; T=2: one period)
+    (1, 4, 1, 3, 0.05, "vacuum", "x", 0),
+    (2, 5, 2, 3, 0.1, "neel", "xy", 0),
+    (3, 6, 1, 4, 0.05, "neel", "circular_left", 1),
+    (6, 1, 1, 2, 0.05, "vacuum", "x", 0),
+    (6, 2, 1, 3, 0.05, "neel", "x", 1),
     (4, 20, 1, 1, 0.0, "vacuum", "x", 0),
     (4, 12, 1, 6, 0.05, "neel", "x", 0),
     (5, 9, 2, 3, 0.1, "vacuum", "circular_left", 0),

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Development A/B of kernel build variants (not the product): bench.py C2 under
+# Development A/B of kernel build variants (not the product): bench.py (C2, or
+# $BENCH_ARGS, e.g. "--config energy") under
 # rocprofv3 --kernel-trace --stats once per library.  Usage (GPU box, repo root):
 #   bash tools/ab_libs.sh <tag> base devlib/libA.so devlib/libB.so ...   (base = lib/libdtc_hip.so)
 set -o pipefail
@@ -10,7 +11,7 @@ i=0
 for lib in "$@"; do
   i=$((i+1)); n=${TAG}_$i
   if [ "$lib" = base ]; then unset DTC_LIB; else export DTC_LIB=$R/$lib; fi
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_$n -o kt -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/ab_$n.json 2> $O/ab_$n.err || { echo "$lib failed"; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_$n -o kt -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS > $O/ab_$n.json 2> $O/ab_$n.err || { echo "$lib failed"; exit 1; }
   python - "$O/ab_$n" "$lib" <<'PY'
 import json, sys, pandas as pd
 d = json.load(open(sys.argv[1] + ".json"))
