@@ -1209,8 +1209,8 @@ static constexpr int kLcTilesPerGroup = 2;
 // sites its mask keeps -- nibble 2 then 1 for even l, 1 then 2 for odd l, one
 // LDS re-layout between them -- with the cone diagonal (conjugated: echo)
 // between consecutive layers; then the probe.  Kicks in Pauli-frame form
-// (dtc_kernels.h): one butterfly variant, no branches per site; a nibble of a
-// layer runs when any of its sites is kicked (identity f = 0 for the others).
+// (dtc_kernels.h): one butterfly variant; a site of a layer runs only when the
+// layer's mask kicks it (scalar branches on the kernel argument).
 // A workgroup takes TPB consecutive tiles of one state: the records and tables
 // are staged once, and the next tile's 16 loads are issued before the current
 // tile's layers (register double buffer: the pass is VALU/LDS-heavy per byte).
@@ -1285,11 +1285,14 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
     constexpr int N = decltype(n_tag)::value;
     constexpr int l = decltype(l_tag)::value;
     constexpr int k0 = kLcSites * l + 4 * (N - 1);
-    if (!((A.lc_mask >> k0) & 0xFull)) return;
-    layer_f<KIND, 0, 0>(v, R.d(0, k0));
-    layer_f<KIND, 0, 1>(v, R.d(0, k0 + 1));
-    layer_f<KIND, 0, 2>(v, R.d(0, k0 + 2));
-    layer_f<KIND, 0, 3>(v, R.d(0, k0 + 3));
+    // per site: the cone leaves most layers' nibbles partly idle (the last
+    // layer kicks j alone), and an idle site's f = 0 butterfly is the
+    // identity; the mask is a kernel argument, so these are scalar branches
+    const int m = (int)((A.lc_mask >> k0) & 0xFull);
+    if (m & 1) layer_f<KIND, 0, 0>(v, R.d(0, k0));
+    if (m & 2) layer_f<KIND, 0, 1>(v, R.d(0, k0 + 1));
+    if (m & 4) layer_f<KIND, 0, 2>(v, R.d(0, k0 + 2));
+    if (m & 8) layer_f<KIND, 0, 3>(v, R.d(0, k0 + 3));
   };
   // cone diagonal after layer l, applied in layout LAY: D_r(x ^ m_l), one
   // table lookup and one complex product per amplitude

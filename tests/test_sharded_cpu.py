@@ -107,7 +107,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, k, q, pipelined=False):
+def _worker(rank, world, port, k, q, pipelined=False, L=8):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -119,7 +119,7 @@ def _worker(rank, world, port, k, q, pipelined=False):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pkg = load_package()
-    spec = _spec(pkg, 8, 5)
+    spec = _spec(pkg, L, 5)
     fwd = pkg.sharded.sharded_forward_pipelined if pipelined else pkg.sharded.sharded_forward
     out = fwd(NumpyShardStepper(_halves), spec, k, inst=0, traj=2, seed=5, rank=rank,
               world=world)
@@ -129,16 +129,17 @@ def _worker(rank, world, port, k, q, pipelined=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k,pipelined", [(1, False), (2, False), (1, True), (2, True)])
-def test_gloo_ranks_match_oracle(pkg, k, pipelined):
+@pytest.mark.parametrize("k,pipelined,L", [(1, False, 8), (2, False, 8), (1, True, 8),
+                                           (2, True, 8), (3, True, 10)])
+def test_gloo_ranks_match_oracle(pkg, k, pipelined, L):
     """Real ranks over gloo: the all_to_all_single exchange, and the pipelined
     driver's per-chunk point-to-point transfers (rank r sends chunk r+i to rank
-    r+i at step i)."""
+    r+i at step i).  World 8 is the C5 rank count: 7 peers at once per slice."""
     world = 1 << k
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q, pipelined))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q, pipelined, L))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -147,7 +148,7 @@ def test_gloo_ranks_match_oracle(pkg, k, pipelined):
         pr.join(timeout=180)
         assert pr.exitcode == 0
     import dataclasses
-    spec = _spec(pkg, 8, 5)
+    spec = _spec(pkg, L, 5)
     one = dataclasses.replace(spec, hs=spec.hs[:1], phis=spec.phis[:1])
     ref = c_oracle.autocorr(one, 1, seed=5, traj_offset=2, want_zsite=True, want_echo=False)
     assert np.abs(got - ref["zsite"][0, 0]).max() < 1e-12
