@@ -24,7 +24,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
 events on the engine's stream over the timed region, all passes that apply
 the diagonal; every rank's rate in per_rank_GBps) and "cpu_baseline" = the
 period-fused CPU restatement (oracle/dtc_oracle.c orc_autocorr_fused) on this
-host's usable cores for a bounded sample, with the CPU model.
+host's usable cores for a bounded sample, with the CPU model.  At 8 ranks
+the line also carries "c5": the C5 configuration (one L=34 state over the 8
+GPUs) measured after the timed C2 region by a nested 8-rank job
+(run_child_ranks), or its error -- it never changes the C2 numbers.
 """
 from __future__ import annotations
 
@@ -331,7 +334,7 @@ def main(argv=None):
     ap.add_argument("--selftest-nested", action="store_true",
                     help="with --spawn-selftest: also run a nested selftest job through "
                          "run_child_ranks (the C5 sub-run's plumbing)")
-    ap.add_argument("--nested-timeout", type=float, default=300.0,
+    ap.add_argument("--nested-timeout", type=float, default=240.0,
                     help="seconds a nested job (the C5 sub-run) may take before it is killed")
     ap.add_argument("--no-c5-subrun", action="store_true",
                     help="c2 at 8 GPUs: skip the C5 (L=34 over 8 GPUs) sub-run that is "
