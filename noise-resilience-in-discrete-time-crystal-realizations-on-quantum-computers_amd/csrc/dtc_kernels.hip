@@ -974,9 +974,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
     }
   };
-  // <X> partials of the 4 sites in register nibble LAY (energy mode): lanes
-  // 0, 16, 32, 48 of each wave end with the wave sums of register bits 0..3
-  // (2 + 1 shuffles halve the 4 values over lane bits 5, 4; 4 more finish).
+  // <X> partials of the 4 sites in register nibble LAY (energy mode): each
+  // thread's 2 Re sum conj(a_0) a_1 over its register pairs of bit q; the wave
+  // reduction (wave_sum_multi<4>: lanes 0, 16, 32, 48 end with the sums of
+  // register bits 0..3) runs after the stores.
   auto pair_sums = [&](auto lay_tag, double (&a)[4], double scale) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -990,20 +991,18 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       a[q] = 2.0 * scale * x;
     }
   };
-  auto measure_x = [&](auto lay_tag, double scale, int slot0) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int wave = t >> 6, lane = t & 63;
-    double a[4];
-    pair_sums(lay_tag, a, scale);
-    const double k = wave_sum_multi<4>(a);
-    if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = k;
-  };
-  // X before the post-kick: each thread's pair sums only; their wave
-  // reductions run after the tile's stores are issued (x_post_finish)
+  // X before a pre- or post-kick nibble: each thread's pair sums only; their
+  // wave reductions run after the tile's stores are issued (the pre-kick sums
+  // stay live across the diagonal: 245 VGPRs, still 2 waves per SIMD)
   double xpost[3][4];
   auto measure_x_post = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
     pair_sums(lay_tag, xpost[LAY], scale);
+  };
+  double xpre[3][4];
+  auto measure_x_pre = [&](auto lay_tag, double scale) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    pair_sums(lay_tag, xpre[LAY], scale);
   };
   // squared share of the global factor carried by the factored kicks of
   // nibble N (records rec0 + 4N .. +3): measuring after them multiplies sums by
@@ -1027,19 +1026,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (RP::pre) {
     double sc = 1.0;
     if constexpr (RP::nIO) {
-      if (x_pre) measure_x(LIO{}, sc, kSlotXPre);
+      if (x_pre) measure_x_pre(LIO{}, sc);
       apply_nibble<RP::IO, KIND>(v, R, 0);
       if (x_pre) sc *= nib_w2(RP::IO, 0);
     }
     if constexpr (RP::n0) {
       exchange<RP::IO, 0>(v, s_tile, t);
-      if (x_pre) measure_x(L0{}, sc, kSlotXPre);
+      if (x_pre) measure_x_pre(L0{}, sc);
       apply_nibble<0, KIND>(v, R, 0);
       if (x_pre) sc *= nib_w2(0, 0);
     }
     if constexpr (RP::nO) {
       exchange<RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, t);
-      if (x_pre) measure_x(LO{}, sc, kSlotXPre);
+      if (x_pre) measure_x_pre(LO{}, sc);
       apply_nibble<RP::O, KIND>(v, R, 0);
     }
   }
@@ -1121,17 +1120,26 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   if constexpr (MC >= 2) {
     // measurement combines after the tile's stores are issued (one barrier)
-    if constexpr (MC == 3 && RP::post) {
-      if (x_post) {
-        const int wave = t >> 6, lane = t & 63;
-        auto finish = [&](auto lay_tag) {
-          constexpr int LAY = decltype(lay_tag)::value;
-          const double k = wave_sum_multi<4>(xpost[LAY]);
-          if ((lane & 15) == 0) s_red[wave][kSlotXPost + 4 * LAY + (lane >> 4)] = k;
-        };
-        if constexpr (RP::nO) finish(LO{});
-        if constexpr (RP::n0) finish(L0{});
-        if constexpr (RP::nIO) finish(LIO{});
+    if constexpr (MC == 3) {
+      const int wave = t >> 6, lane = t & 63;
+      auto finish = [&](auto lay_tag, double (&xs)[3][4], int slot0) {
+        constexpr int LAY = decltype(lay_tag)::value;
+        const double k = wave_sum_multi<4>(xs[LAY]);
+        if ((lane & 15) == 0) s_red[wave][slot0 + 4 * LAY + (lane >> 4)] = k;
+      };
+      if constexpr (RP::pre) {
+        if (x_pre) {
+          if constexpr (RP::nIO) finish(LIO{}, xpre, kSlotXPre);
+          if constexpr (RP::n0) finish(L0{}, xpre, kSlotXPre);
+          if constexpr (RP::nO) finish(LO{}, xpre, kSlotXPre);
+        }
+      }
+      if constexpr (RP::post) {
+        if (x_post) {
+          if constexpr (RP::nO) finish(LO{}, xpost, kSlotXPost);
+          if constexpr (RP::n0) finish(L0{}, xpost, kSlotXPost);
+          if constexpr (RP::nIO) finish(LIO{}, xpost, kSlotXPost);
+        }
       }
     }
     if (zc_lay >= 0 || x_pre || x_post) {
