@@ -105,7 +105,14 @@ def cpu_baseline(spec, n_traj, T_sample, threads=None, t_offset=0):
 def read_traffic(bytes_per_launch, suffix="_pmc.json"):
     """HBM bytes per launch of the RZZ kernel from the latest committed PMC
     summary named *<suffix> (tools/pmc_summary.py output), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)))
+    import re
+
+    def tag_order(path):
+        # profile tags run r1a .. r1z, r2a .. r2z, r2aa, r2ab, ...: (round, length, letters)
+        m = re.match(r"r(\d+)([a-z]+)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, path)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)), key=tag_order)
     if not files:
         return None, None
     with open(files[-1]) as f:
