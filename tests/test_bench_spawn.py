@@ -47,6 +47,24 @@ def test_nested_job_from_ranks():
     assert d["nested"]["rank_sum"] == 1
 
 
+def test_nested_job_under_torchrun():
+    """The driver launches N>1 under torch.distributed.run: the nested job must
+    host its own rendezvous (torchrun's agent-store variables are dropped)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    port = str(29000 + os.getpid() % 1000)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        port, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--spawn-selftest",
+                        "--selftest-nested"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["nested"]["n_gpus"] == 2 and d["nested"]["value"] == 2
+
+
 def test_nested_job_hang_is_contained():
     """A nested rank that never finishes is killed at the timeout; the outer
     job still prints its line, with the nested job's error."""
