@@ -459,7 +459,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
                      int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
                      const dtc::KickRec* recs = nullptr, int meas_parts = 0,
-                     int no_store = 0) {
+                     int no_store = 0, const int64_t* basis = nullptr) {
   const int shape = pass_shape(ps);
   if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
   const int kind = pass_kind(rc, ps, shape);
@@ -526,6 +526,9 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   }
   A.src = src;
   A.dst = dst;
+  // the source is the basis state (synthesised by the kernel): kick-only passes
+  if (basis && shape != dtc::kShapeK) return fail(DTC_EINVAL, "internal: basis source on a non-kick pass");
+  A.basis = basis;
   A.c = g.c;
   A.s = g.s;
   A.tile_bits_mid = g.s - g.c;
@@ -571,6 +574,7 @@ struct Launch {
   double* meas_out;
   int64_t meas_stride;
   int no_store = 0;  // the pass's output is never read again (last pass of an echo chain)
+  const int64_t* basis = nullptr;  // first pass of a sweep: src = the basis states (synthesised)
 };
 
 int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
@@ -594,9 +598,24 @@ int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
       const Launch& l = L[i0 + i];
       DTC_TRY(launch_pass_spec(ctx, rc, batch_start, batch, l.ps, l.src, l.dst, l.meas_mode,
                                l.meas_at_end, l.n_obs, l.meas_out, l.meas_stride,
-                               P.out + i * batch * dtc::kRecPerState, 0, l.no_store));
+                               P.out + i * batch * dtc::kRecPerState, 0, l.no_store, l.basis));
     }
   }
+  return DTC_OK;
+}
+
+// The basis states of a batch (masks already in ctx->basis) as the source of
+// its schedule: a first pass that only kicks forms them in registers (no
+// zero-fill of F, no read of it); any other first pass reads F, filled here.
+template <class LaunchT>
+int basis_source(dtc_ctx* ctx, std::vector<LaunchT>& sched, double2* F, int64_t len, int nb) {
+  if (!sched.empty() && pass_shape(sched[0].ps) == dtc::kShapeK &&
+      std::getenv("DTC_NO_BASIS_SYNTH") == nullptr) {
+    sched[0].basis = (const int64_t*)ctx->basis.p;
+    return DTC_OK;
+  }
+  DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * len * 16, ctx->stream));
+  DTC_HIP(dtc::launch_set_basis(F, len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
   return DTC_OK;
 }
 
@@ -1195,8 +1214,6 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     if (!use_prefix) {
       DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
                              hipMemcpyHostToDevice, ctx->stream));
-      DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
-      DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
     }
     DTC_HIP(hipMemsetAsync(ctx->vals_f.p, 0, (size_t)nb * T * n_obs_f * sizeof(double),
                            ctx->stream));
@@ -1267,6 +1284,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         sched.back().no_store = 1;
       }
     }
+    if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
@@ -1543,6 +1561,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     PassSpec ps;
     int parts, t_mid, t_pre;
     bool xbasis;
+    const int64_t* basis = nullptr;
   };
   std::vector<EPass> sched;
   if (P > 0 && dv) {
@@ -1603,8 +1622,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     double* vals = (double*)ctx->vals_f.p;
     DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
                            hipMemcpyHostToDevice, ctx->stream));
-    DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
-    DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
     DTC_HIP(hipMemsetAsync(vals, 0, (size_t)nb * T * n_v * sizeof(double), ctx->stream));
     const int64_t vs = (int64_t)T * n_v;
     // kick records of the schedule's passes: one prep launch per segment
@@ -1629,7 +1647,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       const dtc::KickRec* recs = (const dtc::KickRec*)ctx->recs.p + (i % seg) * nb * dtc::kRecPerState;
       DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, e.ps, F, F,
                                e.parts ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_obs, nullptr,
-                               0, recs, e.parts));
+                               0, recs, e.parts, 0, e.basis));
       if (e.parts & dtc::kPartZ)
         DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb, vals + (size_t)e.t_mid * n_v, vs,
                                    0, (e.parts & dtc::kPartXPost) ? 3 * L : 2 * L, 1));

@@ -191,6 +191,8 @@ struct PassArgs {
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]
+  const int64_t* basis;    // kick-only passes: non-null = the source is the basis state
+                           // |basis[b]> (synthesised in registers: src is not read)
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
 

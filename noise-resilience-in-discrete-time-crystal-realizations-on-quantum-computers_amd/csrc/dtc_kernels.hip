@@ -733,7 +733,17 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const bool ofs32 = RP::IO == 2 || (c > 11 ? 11 : s + 11 - c) <= 27;
   auto tile_ofs = [&](int r) -> int64_t { return (M.tbase | M.rel(r << (4 * RP::IO))) << 4; };
   double2 v[kRegs];
-  {
+  bool synth = false;
+  if constexpr (SHAPE == kShapeK) synth = A.basis != nullptr;
+  if (synth) {
+    // the first pass of a sweep: the source is the basis state |basis[b]>,
+    // formed in registers (no zero-fill of the batch, no read of it)
+    const int64_t m = A.basis[b];
+    const int64_t x0 = M.tbase | M.rel(ybase<RP::IO>(t));
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r)
+      v[r] = make_double2((x0 | M.rel(r << (4 * RP::IO))) == m ? 1.0 : 0.0, 0.0);
+  } else {
     const char* src = (const char*)(A.src + b * A.state_len);
     if (ofs32) {
 #pragma unroll
