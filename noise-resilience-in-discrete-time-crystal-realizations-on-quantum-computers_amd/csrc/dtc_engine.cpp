@@ -1562,6 +1562,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     int parts, t_mid, t_pre;
     bool xbasis;
     const int64_t* basis = nullptr;
+    int no_store = 0;
   };
   std::vector<EPass> sched;
   if (P > 0 && dv) {
@@ -1612,6 +1613,10 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       for (int g = 0; g < G; ++g)
         if (t + pr->t_offset >= 1 && !x_done[(size_t)t * G + g])
           return fail(DTC_EINVAL, "internal: dtc_energy left an X group unmeasured");
+    // the extra kick layer's pass only measures X: its state is never read
+    if (sched.size() >= 2 && pass_shape(sched.back().ps) == dtc::kShapeK &&
+        (sched.back().parts & dtc::kPartXPre) && !(sched.back().parts & dtc::kPartZ))
+      sched.back().no_store = 1;
   }
 
   for (int64_t bs = 0; bs < S; bs += B) {
@@ -1647,7 +1652,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       const dtc::KickRec* recs = (const dtc::KickRec*)ctx->recs.p + (i % seg) * nb * dtc::kRecPerState;
       DTC_TRY(launch_pass_spec(ctx, rc, bs, nb, e.ps, F, F,
                                e.parts ? dtc::kMeasEnergy : dtc::kMeasNone, 0, n_obs, nullptr,
-                               0, recs, e.parts, 0, e.basis));
+                               0, recs, e.parts, e.no_store, e.basis));
       if (e.parts & dtc::kPartZ)
         DTC_TRY(launch_reduce_prof(ctx, pl.n_tiles, n_obs, nb, vals + (size_t)e.t_mid * n_v, vs,
                                    0, (e.parts & dtc::kPartXPost) ? 3 * L : 2 * L, 1));

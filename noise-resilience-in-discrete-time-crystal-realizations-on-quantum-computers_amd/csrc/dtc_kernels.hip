@@ -1210,6 +1210,12 @@ DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
 DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
 DTC_DEFINE_FINAL(dtc_kick_final, kShapeK)
 #undef DTC_DEFINE_FINAL
+// The energy sweep's last pass (one kick layer past the last period, for the
+// X of its group at the last time point): measures, stores nothing.
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kick_xfinal(PassArgs A) {
+  pass_body<kShapeK, NIBS, KIND, 3, true>(A);
+}
 template <int NIBS, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
   pass_body<kShapeD, NIBS, kKindRX, MC>(A);
@@ -1422,8 +1428,12 @@ template <int NIBS, int KIND, int MC>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
   if (a.no_store) {
-    if constexpr (MC != 1) {
-      return hipErrorInvalidValue;  // only probe passes end an echo chain
+    if constexpr (MC == 3) {
+      if (shape != kShapeK) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((dtc_kick_xfinal<NIBS, KIND>), grid, block, 0, stream, a);
+      return hipGetLastError();
+    } else if constexpr (MC != 1) {
+      return hipErrorInvalidValue;  // probe passes end an echo chain, energy sweeps a kick pass
     } else {
       switch (shape) {
         case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
