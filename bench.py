@@ -47,9 +47,11 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0    # float4 copy measured (same table)
-BOX_COPY_GBS = 5715.0        # best read+write stream measured on this part (in place, 4 x 16 B
-                             # per lane; tools/hbm_ceiling.hip, profiles/r2d_hbm_ceiling.txt:
+BOX_COPY_GBS = 5715.0        # best copy-kernel read+write stream measured on this part (in place,
+                             # 4 x 16 B per lane; tools/hbm_ceiling.hip, profiles/r2d_hbm_ceiling.txt:
                              # read alone 7.0-7.3 TB/s, write alone 5.2 TB/s)
+BEST_RW_PASS_GBS = 6080.0    # best read+write rate any pass kernel reached on this part: a
+                             # 12-site kick-only pass over L=28 states (profiles/r2ak_state_size.txt)
 METRIC = "Floquet-periods×instances/sec at L=20; RZZ-kernel HBM GB/s vs peak"
 
 
@@ -540,6 +542,7 @@ def main(argv=None):
             "frac": achieved / HBM_PEAK_GBS,
             "frac_of_measured_copy": achieved / HBM_MEASURED_GBS,
             "frac_of_box_copy": achieved / BOX_COPY_GBS,
+            "frac_of_best_rw_pass": achieved / BEST_RW_PASS_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": launch_bytes,
