@@ -1357,13 +1357,12 @@ int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     double2* F = (double2*)ctx->prefix.p + (size_t)bs * pl.len;
     DTC_HIP(hipMemcpyAsync(ctx->basis.p, ctx->prefix_masks.data() + bs, nb * sizeof(int64_t),
                            hipMemcpyHostToDevice, ctx->stream));
-    DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * pl.len * 16, ctx->stream));
-    DTC_HIP(dtc::launch_set_basis(F, pl.len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
     Chain fw = forward_chain(pl, 1, n_periods, dtc::kStreamForward);
     fw.post_after_d = !rc.device;
     std::vector<Launch> sched;
     while (!fw.done())
       sched.push_back(Launch{next_pass(fw), F, F, dtc::kMeasNone, 0, 2, nullptr, 0});
+    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipStreamSynchronize(ctx->stream));  // the staged pass list is reused
   }
