@@ -488,6 +488,27 @@ __device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, i
   for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y<TO>(t, r))];
 }
 
+// The same re-layout through a 32 KiB buffer, real parts then imaginary parts
+// (8-B slots, swizzle y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4), half-wave
+// conflict-free): half the LDS, so three workgroups fit a CU; two more
+// barriers (the imaginary writes reuse the slots the real reads just left).
+__device__ __forceinline__ int lds_slot8(int y) { return y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4); }
+template <int FROM, int TO>
+__device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t) {
+  if (FROM == TO) return;
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) s_half[lds_slot8(tile_y<FROM>(t, r))] = v[r].x;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) v[r].x = s_half[lds_slot8(tile_y<TO>(t, r))];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) s_half[lds_slot8(tile_y<FROM>(t, r))] = v[r].y;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) v[r].y = s_half[lds_slot8(tile_y<TO>(t, r))];
+}
+
 __device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chunks, int64_t x) {
   double2 ph = s_chunk[x & 63];
   for (int k = 1; k < n_chunks; ++k) {
@@ -1238,10 +1259,11 @@ static constexpr int kLcTilesPerGroup = 2;
 // A workgroup takes TPB consecutive tiles of one state: the records and tables
 // are staged once, and the next tile's 16 loads are issued before the current
 // tile's layers (register double buffer: the pass is VALU/LDS-heavy per byte).
-template <int KIND, int TPB>
+template <int KIND, int TPB, bool SPLIT = false>
 __device__ __forceinline__ void lc_body(const PassArgs& A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
-  __shared__ double2 s_tile[kTile];
+  __shared__ double2 s_tile[SPLIT ? 1 : kTile];
+  __shared__ double s_half[SPLIT ? kTile : 1];
   __shared__ double2 s_cone[kLcTab];
   __shared__ double s_red[kThreads / 64][2];
   const int t = threadIdx.x;
@@ -1337,35 +1359,40 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
   };
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
+  auto lc_xch_impl = [&](double2 (&v)[kRegs], auto from_tag, auto to_tag) {
+    constexpr int F = decltype(from_tag)::value, T = decltype(to_tag)::value;
+    if constexpr (SPLIT) exchange_split<F, T>(v, s_half, t);
+    else exchange<F, T>(v, s_tile, t);
+  };
   // one tile, its amplitudes in v (layout 2)
   auto process = [&](double2 (&v)[kRegs], int64_t tile) {
     M.tbase = tbase_of(tile);
     // layer 0: nibble 2 (layout 2), re-layout, nibble 1 (layout 1), D
     kick(v, L2{}, std::integral_constant<int, 0>{});
-    exchange<2, 1>(v, s_tile, t);
+    lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
     kick(v, L1{}, std::integral_constant<int, 0>{});
     if (nl > 1) {  // layer 1: 1 -> 2
       diag(v, L1{}, 0);
       kick(v, L1{}, std::integral_constant<int, 1>{});
-      exchange<1, 2>(v, s_tile, t);
+      lc_xch_impl(v, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
       kick(v, L2{}, std::integral_constant<int, 1>{});
     }
     if (nl > 2) {  // layer 2: 2 -> 1
       diag(v, L2{}, 1);
       kick(v, L2{}, std::integral_constant<int, 2>{});
-      exchange<2, 1>(v, s_tile, t);
+      lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
       kick(v, L1{}, std::integral_constant<int, 2>{});
     }
     if (nl > 3) {  // layer 3: 1 -> 2
       diag(v, L1{}, 2);
       kick(v, L1{}, std::integral_constant<int, 3>{});
-      exchange<1, 2>(v, s_tile, t);
+      lc_xch_impl(v, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
       kick(v, L2{}, std::integral_constant<int, 3>{});
     }
     if (nl > 4) {  // layer 4: 2 -> 1
       diag(v, L2{}, 3);
       kick(v, L2{}, std::integral_constant<int, 4>{});
-      exchange<2, 1>(v, s_tile, t);
+      lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
       kick(v, L1{}, std::integral_constant<int, 4>{});
     }
     // probe: layout 1 after an odd number of layers, 2 after an even number;
@@ -1422,6 +1449,13 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
 template <int KIND, int TPB>
 __global__ __launch_bounds__(kThreads, 2) void dtc_lc_final(PassArgs A) {
   lc_body<KIND, TPB>(A);
+}
+// One tile per workgroup, re-layouts through half the LDS: three per CU (the
+// pass is bound by its per-workgroup chain, so a third chain per CU pays more
+// than the two extra barriers per re-layout cost; the default)
+template <int KIND>
+__global__ __launch_bounds__(kThreads, 3) void dtc_lc_final_split(PassArgs A) {
+  lc_body<KIND, 1, true>(A);
 }
 
 template <int NIBS, int KIND, int MC>
@@ -1508,6 +1542,16 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
     // several tiles per workgroup (register double buffer) when they divide the state
     int tpb = kLcTilesPerGroup;
     if (const char* e = std::getenv("DTC_LC_TPB")) tpb = std::atoi(e);  // development A/B
+    // default: one tile per workgroup, re-layouts through half the LDS, three
+    // workgroups per CU (r2ar: 6.15 -> 5.42 ms); DTC_LC_SPLIT=0 keeps the
+    // 64 KiB exchange and DTC_LC_TPB tiles per workgroup (development A/B)
+    const char* split_env = std::getenv("DTC_LC_SPLIT");
+    if (!(split_env && split_env[0] == '0')) {
+      if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((kind == kKindRX ? dtc_lc_final_split<kKindRX> : dtc_lc_final_split<kKindRY>),
+                         grid, dim3(kThreads), 0, stream, a);
+      return hipGetLastError();
+    }
     while (tpb > 1 && n_tiles % tpb) tpb >>= 1;
     if (tpb != 1 && tpb != 2 && tpb != 4) tpb = 1;
     grid.x = n_tiles / tpb;
