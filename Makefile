@@ -5,19 +5,40 @@ CC      ?= gcc
 PKG     := noise-resilience-in-discrete-time-crystal-realizations-on-quantum-computers_amd
 ARCH    ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -Wall -Wno-unused-result
+HIPCFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+# CPU oracle (test infrastructure): portable build, plus an x86-64-v3 build
+# that is loaded only on hosts with those features.
+ORACLE_MARCH ?= x86-64-v2
+OBJDIR  := build/obj
 
 LIB     := $(PKG)/lib/libdtc_hip.so
 ORACLE  := oracle/liboracle.so
+ORACLE3 := oracle/liboracle_v3.so
 SRCS    := $(PKG)/csrc/dtc_kernels.hip $(PKG)/csrc/dtc_engine.cpp
 HDRS    := $(PKG)/csrc/dtc_kernels.h $(PKG)/csrc/dtc_rng.h include/dtc.h
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ORACLE) $(ORACLE3)
 
-$(LIB): $(SRCS) $(HDRS)
+# the two translation units compile separately (the kernels take minutes, the
+# host engine seconds), then link into the one product library
+$(OBJDIR)/dtc_kernels.o: $(PKG)/csrc/dtc_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
+
+$(OBJDIR)/dtc_engine.o: $(PKG)/csrc/dtc_engine.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
+
+$(LIB): $(OBJDIR)/dtc_kernels.o $(OBJDIR)/dtc_engine.o
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) $(SRCS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared $^ -o $@
 
 $(ORACLE): oracle/dtc_oracle.c
+	$(CC) -O3 -march=$(ORACLE_MARCH) -fopenmp -fPIC -shared -std=c11 -Wall $< -o $@ -lm
+
+# the same source for AVX2/FMA hosts: oracle/c_oracle.py loads it only when
+# /proc/cpuinfo lists the x86-64-v3 features (the bench's CPU baseline)
+$(ORACLE3): oracle/dtc_oracle.c
 	$(CC) -O3 -march=x86-64-v3 -fopenmp -fPIC -shared -std=c11 -Wall $< -o $@ -lm
 
 resource-usage: $(SRCS) $(HDRS)
@@ -30,6 +51,6 @@ build/libdtc_timing.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DDTC_PHASE_TIMING=3 $(SRCS) -o $@
 
 clean:
-	rm -f $(LIB) $(ORACLE)
+	rm -f $(LIB) $(ORACLE) $(ORACLE3) $(OBJDIR)/*.o
 
 .PHONY: all clean resource-usage

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 6
+#define DTC_ABI_VERSION 7
 
 /* error codes */
 #define DTC_OK 0
@@ -116,6 +116,11 @@ typedef struct dtc_device_noise {
 /* Context management. device = HIP device ordinal. */
 int dtc_open(int32_t device, dtc_ctx** out);
 int dtc_close(dtc_ctx* ctx);
+/* Free the ctx's batch work buffers (state batches, partial sums, kick
+ * records; the next call re-allocates what it needs) after waiting for its
+ * stream -- e.g. before the caller allocates one 256 GiB sharded state on the
+ * same device.  The forward prefix (dtc_prefix_*) is kept. */
+int dtc_release_buffers(dtc_ctx* ctx);
 const char* dtc_last_error(void);
 int32_t dtc_abi_version(void);
 
@@ -217,6 +222,18 @@ int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise*
                          uint64_t pre_mask, int32_t chunk_bits, int32_t slice_bits,
                          int32_t slice, double* state);
 
+/* Virtual ranks only (one process holds every shard: n_shards = 2^n_global,
+ * first_rank = 0): the period's all-to-all for slice `slice`, in place.  With
+ * chunk bits = the top n_global local bits and slice bits = the next
+ * slice_bits, piece (shard r, chunk c, slice) trades places with piece
+ * (shard c, chunk r, slice) for every r != c -- what the 2^n_global ranks'
+ * exchange of that slice does over xGMI, without a second state buffer (an
+ * L=34 state, 256 GiB, then fits one MI355X).  Asynchronous, ctx stream, one
+ * launch; 2^(n_local - n_global - slice_bits) >= 4096.  No reference call
+ * site (the reference caps L at 20, fast.py:177-178). */
+int dtc_shard_exchange_slice(dtc_ctx* ctx, const dtc_shard* shard, int32_t slice_bits,
+                             int32_t slice, double* state);
+
 /* The ctx's HIP stream (hipStream_t), for ordering host-side collectives
  * against the asynchronous entry points; and a wait for everything on it. */
 int dtc_get_stream(dtc_ctx* ctx, void** stream);
@@ -278,7 +295,12 @@ int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_no
 #define DTC_KERNEL_REDUCE 2    /* per-state observable reduction             */
 #define DTC_KERNEL_INIT 3      /* basis-state preparation                    */
 #define DTC_KERNEL_FINAL_PASS 4 /* last pass of an echo chain: measure, no store */
-#define DTC_KERNEL_KINDS 5
+#define DTC_KERNEL_EXCHANGE 5  /* virtual ranks' in-place slice exchange        */
+#define DTC_KERNEL_KINDS 6
+/* total_bytes = algorithmic HBM bytes of the launches: 32 B per amplitude for a
+ * pass that reads and stores its state, 16 B for one that only reads
+ * (measure-only) or only stores (the first pass of a sweep, which forms the
+ * basis states in registers), 32 B per amplitude an exchange moves. */
 int dtc_set_profiling(dtc_ctx* ctx, int32_t on);
 int dtc_kernel_stats(dtc_ctx* ctx, int32_t kind, int64_t* launches,
                      double* total_ms, double* total_bytes);

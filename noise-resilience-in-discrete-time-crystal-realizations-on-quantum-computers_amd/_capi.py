@@ -14,13 +14,15 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
-KERNEL_KINDS = 5  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass
-ABI_VERSION = 6  # DTC_ABI_VERSION of include/dtc.h this binding matches
+KERNEL_KINDS = 6  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass,
+                  # virtual-rank exchange
+ABI_VERSION = 7  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
     "dtc_open",
     "dtc_close",
+    "dtc_release_buffers",
     "dtc_last_error",
     "dtc_abi_version",
     "dtc_autocorr",
@@ -40,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "dtc_prefix_release",
     "dtc_shard_step_async",
     "dtc_shard_kick_slice",
+    "dtc_shard_exchange_slice",
     "dtc_get_stream",
     "dtc_synchronize",
 )
@@ -48,11 +51,15 @@ KERNEL_LO_PASS = 0
 KERNEL_HI_PASS = 1
 KERNEL_REDUCE = 2
 KERNEL_INIT = 3
+KERNEL_FINAL_PASS = 4
+KERNEL_EXCHANGE = 5
 KERNEL_NAMES = {
     KERNEL_LO_PASS: "pass_kernel<diag>  (fused RZZ+RZ diagonal + sites 0..11 kick)",
     KERNEL_HI_PASS: "pass_kernel<none>  (kick on sites >= 12)",
     KERNEL_REDUCE: "reduce_kernel",
     KERNEL_INIT: "set_basis_kernel",
+    KERNEL_FINAL_PASS: "dtc_*_final / dtc_lc_final_split (measure only, no store)",
+    KERNEL_EXCHANGE: "exchange_swap_kernel (virtual ranks' in-place slice exchange)",
 }
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -141,9 +148,11 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         # torch's later device initialisation in the same process fails ("No
         # HIP GPUs are available").  Importing torch first makes this
         # library's libamdhip64.so.7 dependency resolve to the loaded copy.
+        # A torch install that fails to import (ImportError, or OSError from a
+        # broken wheel) only costs that ordering: the library still loads.
         try:
             import torch  # noqa: F401
-        except ImportError:
+        except Exception:  # noqa: BLE001
             pass
         lib = ctypes.CDLL(p)
         lib.dtc_abi_version.restype = ctypes.c_int32
@@ -155,6 +164,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         P = ctypes.POINTER
         lib.dtc_open.argtypes = [ctypes.c_int32, P(ctypes.c_void_p)]
         lib.dtc_close.argtypes = [ctypes.c_void_p]
+        lib.dtc_release_buffers.argtypes = [ctypes.c_void_p]
         lib.dtc_last_error.restype = ctypes.c_char_p
         lib.dtc_abi_version.restype = ctypes.c_int32
         lib.dtc_autocorr.argtypes = [
@@ -192,6 +202,9 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcShard), ctypes.c_uint64,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
             ctypes.c_int32, ctypes.c_void_p,
+        ]
+        lib.dtc_shard_exchange_slice.argtypes = [
+            ctypes.c_void_p, P(DtcShard), ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
         ]
         lib.dtc_get_stream.argtypes = [ctypes.c_void_p, P(ctypes.c_void_p)]
         lib.dtc_synchronize.argtypes = [ctypes.c_void_p]

@@ -98,9 +98,10 @@ struct dtc_ctx {
   // the asynchronous steps of a sweep never re-upload from host memory
   struct ShardTables {
     uint64_t key = 0;
-    DevBuf diag, sitemap;
+    DevBuf diag;
   };
   std::vector<ShardTables> shard_cache;  // most recent last, at most 4
+  std::vector<ShardTables> shard_maps;   // bit -> site maps (diag = the map), at most 4
   DevBuf shard_kick;
   uint64_t shard_kick_key = 0;
 };
@@ -555,8 +556,10 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream));
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
-    ctx->pending.push_back(Pending{kernel, e0, e1,
-                                   (no_store ? 16.0 : 32.0) * (double)((int64_t)1 << A.L_eff) * batch});
+    // algorithmic bytes: a read and a store per amplitude, or one of them
+    // (measure-only passes store nothing, a basis-synthesising pass reads nothing)
+    const double per_amp = (no_store || basis) ? 16.0 : 32.0;
+    ctx->pending.push_back(Pending{kernel, e0, e1, per_amp * (double)((int64_t)1 << A.L_eff) * batch});
   }
   if (meas_mode != dtc::kMeasNone && meas_out)
     DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
@@ -985,8 +988,25 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->dev_thr);
   release(ctx->dev_jump);
   release(ctx->dev_kraus);
+  for (auto& e : ctx->shard_cache) release(e.diag);
+  for (auto& e : ctx->shard_maps) release(e.diag);
+  release(ctx->shard_kick);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  return DTC_OK;
+}
+
+int dtc_release_buffers(dtc_ctx* ctx) {
+  if (!ctx) return fail(DTC_EINVAL, "null ctx");
+  DTC_HIP(hipSetDevice(ctx->device));
+  DTC_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->prof) DTC_TRY(resolve_pending(ctx));
+  release(ctx->F);
+  release(ctx->E);
+  release(ctx->partial);
+  release(ctx->recs);
+  release(ctx->recs1);
+  release(ctx->pk);
   return DTC_OK;
 }
 
@@ -1771,45 +1791,48 @@ uint64_t fnv(uint64_t h, const void* p, size_t n) {
   return h;
 }
 
-// Device tables of one shard bit map (effective diagonal per held shard and
-// the bit -> site map) and the logical kick table, built once and cached.
-int shard_tables(dtc_ctx* ctx, const dtc_problem* pr, const dtc_shard* sh, int inst,
-                 const Plan& pl, RunCfg& rc) {
-  const int L = pr->L, nl = sh->n_local, B = sh->n_shards;
-  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
-  uint64_t key = 1469598103934665603ull;
-  key = fnv(key, &L, sizeof(L));
-  key = fnv(key, &sh->n_local, sizeof(int32_t) * 4);
-  key = fnv(key, sh->site_of, sizeof(int32_t) * L);
-  key = fnv(key, &inst, sizeof(inst));
-  key = fnv(key, pr->h + (size_t)inst * L, sizeof(double) * L);
-  if (L > 1) key = fnv(key, pr->phi + (size_t)inst * (L - 1), sizeof(double) * (L - 1));
-  auto& cache = ctx->shard_cache;
-  int hit = -1;
-  for (size_t i = 0; i < cache.size(); ++i)
-    if (cache[i].key == key) hit = (int)i;
-  if (hit < 0) {
-    std::vector<double> he((size_t)B * nl), pe((size_t)B * std::max(nl - 1, 1)), ca(B);
-    for (int b = 0; b < B; ++b)
-      shard_chain(pr, sh, inst, sh->first_rank + b, he.data() + (size_t)b * nl,
-                  pe.data() + (size_t)b * std::max(nl - 1, 1), &ca[b]);
-    std::vector<double> dt;
-    build_diag_tables(pl, B, he.data(), pe.data(), dt, ca.data());
-    if (cache.size() >= 4) {
-      DTC_HIP(hipStreamSynchronize(ctx->stream));  // the evicted tables may be in use
-      release(cache.front().diag);
-      release(cache.front().sitemap);
-      cache.erase(cache.begin());
+// A small device-table cache (most recent last, at most 4 entries): the entry
+// for `key`, built by `fill` (host bytes) on a miss.  Evicting an entry waits
+// for the stream (its table may be in use); a sweep alternates two bit maps,
+// so that happens only when a caller switches problems.
+template <class Fill>
+int cached_table(dtc_ctx* ctx, std::vector<dtc_ctx::ShardTables>& cache, uint64_t key,
+                 Fill fill, const void** out) {
+  for (auto& e : cache)
+    if (e.key == key) {
+      *out = e.diag.p;
+      return DTC_OK;
     }
-    cache.emplace_back();
-    auto& e = cache.back();
-    DTC_TRY(ensure(e.diag, dt.size() * sizeof(double)));
-    DTC_TRY(ensure(e.sitemap, 64 * sizeof(int)));
-    DTC_HIP(hipMemcpy(e.diag.p, dt.data(), dt.size() * sizeof(double), hipMemcpyHostToDevice));
-    DTC_HIP(hipMemcpy(e.sitemap.p, sh->site_of, 64 * sizeof(int), hipMemcpyHostToDevice));
-    e.key = key;
-    hit = (int)cache.size() - 1;
+  std::vector<double> host;
+  fill(host);
+  if (cache.size() >= 4) {
+    DTC_HIP(hipStreamSynchronize(ctx->stream));
+    release(cache.front().diag);
+    cache.erase(cache.begin());
   }
+  cache.emplace_back();
+  auto& e = cache.back();
+  DTC_TRY(ensure(e.diag, host.size() * sizeof(double)));
+  DTC_HIP(hipMemcpy(e.diag.p, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice));
+  e.key = key;
+  *out = e.diag.p;
+  return DTC_OK;
+}
+
+// The kick-side tables of a shard bit map: the bit -> site map (cached per
+// map) and the logical kick table.  dtc_shard_kick_slice needs only these.
+int shard_kick_tables(dtc_ctx* ctx, const dtc_problem* pr, const dtc_shard* sh, RunCfg& rc) {
+  const int L = pr->L;
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  uint64_t mkey = fnv(1469598103934665603ull, sh->site_of, sizeof(int32_t) * 64);
+  const void* map = nullptr;
+  DTC_TRY(cached_table(ctx, ctx->shard_maps, mkey,
+                       [&](std::vector<double>& h) {
+                         h.assign(32, 0.0);  // 64 int32 in 32 doubles
+                         std::memcpy(h.data(), sh->site_of, 64 * sizeof(int32_t));
+                       },
+                       &map));
+  rc.site_of = (const int*)map;
   const size_t kb = (size_t)n_rows * L * pr->n_sub * 8 * sizeof(double);
   uint64_t kkey = fnv(1469598103934665603ull, &kb, sizeof(kb));
   kkey = fnv(kkey, pr->kick, kb);
@@ -1819,10 +1842,36 @@ int shard_tables(dtc_ctx* ctx, const dtc_problem* pr, const dtc_shard* sh, int i
     DTC_HIP(hipMemcpy(ctx->shard_kick.p, pr->kick, kb, hipMemcpyHostToDevice));
     ctx->shard_kick_key = kkey;
   }
-  rc.diag_tab = (const double2*)cache[hit].diag.p;
-  rc.site_of = (const int*)cache[hit].sitemap.p;
   rc.kick_tab = (const double2*)ctx->shard_kick.p;
   return DTC_OK;
+}
+
+// Device tables of one shard bit map and instance: the effective diagonal per
+// held shard (cached per map, instance and angles) plus the kick-side tables.
+int shard_tables(dtc_ctx* ctx, const dtc_problem* pr, const dtc_shard* sh, int inst,
+                 const Plan& pl, RunCfg& rc) {
+  const int L = pr->L, nl = sh->n_local, B = sh->n_shards;
+  uint64_t key = 1469598103934665603ull;
+  key = fnv(key, &L, sizeof(L));
+  key = fnv(key, &sh->n_local, sizeof(int32_t) * 4);
+  key = fnv(key, sh->site_of, sizeof(int32_t) * L);
+  key = fnv(key, &inst, sizeof(inst));
+  key = fnv(key, pr->h + (size_t)inst * L, sizeof(double) * L);
+  if (L > 1) key = fnv(key, pr->phi + (size_t)inst * (L - 1), sizeof(double) * (L - 1));
+  const void* tab = nullptr;
+  DTC_TRY(cached_table(ctx, ctx->shard_cache, key,
+                       [&](std::vector<double>& dt) {
+                         std::vector<double> he((size_t)B * nl),
+                             pe((size_t)B * std::max(nl - 1, 1)), ca(B);
+                         for (int b = 0; b < B; ++b)
+                           shard_chain(pr, sh, inst, sh->first_rank + b,
+                                       he.data() + (size_t)b * nl,
+                                       pe.data() + (size_t)b * std::max(nl - 1, 1), &ca[b]);
+                         build_diag_tables(pl, B, he.data(), pe.data(), dt, ca.data());
+                       },
+                       &tab));
+  rc.diag_tab = (const double2*)tab;
+  return shard_kick_tables(ctx, pr, sh, rc);
 }
 
 int shard_check_common(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
@@ -1982,7 +2031,7 @@ int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* n
   DTC_HIP(hipSetDevice(ctx->device));
   RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
   const Plan& pl = rc.pl;
-  DTC_TRY(shard_tables(ctx, pr, sh, 0, pl, rc));
+  DTC_TRY(shard_kick_tables(ctx, pr, sh, rc));  // kick-only passes read no diagonal
   // one launch: the slice of every (shard, chunk) piece is a 2^nsub-amplitude
   // state, pieces 2^(nl - chunk_bits) apart (the same trajectory: identical
   // kick records for every piece)
@@ -1999,6 +2048,35 @@ int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* n
                            (uint32_t)period, skip_bits(G, pre_mask)};
     DTC_TRY(launch_pass_spec(ctx, rc, 0, (int)n_pieces, ps, base, base, dtc::kMeasNone, 1, 2,
                              nullptr, 0));
+  }
+  return DTC_OK;
+}
+
+int dtc_shard_exchange_slice(dtc_ctx* ctx, const dtc_shard* sh, int32_t slice_bits,
+                             int32_t slice, double* state) {
+  if (!ctx || !sh || !state) return fail(DTC_EINVAL, "null ctx/shard/state");
+  const int nl = sh->n_local, k = sh->n_global;
+  if (k < 1 || k > 6 || nl < 2 * k || nl > 40)
+    return fail(DTC_EINVAL, "need 1 <= n_global <= 6 and n_local >= 2 n_global");
+  if (sh->n_shards != (1 << k) || sh->first_rank != 0)
+    return fail(DTC_EINVAL, "the in-place exchange needs every shard in this buffer");
+  if (slice_bits < 0 || nl - k - slice_bits < dtc::kTileBits)
+    return fail(DTC_EINVAL, "slice_bits must leave >= 12 bits per slice");
+  if (slice < 0 || slice >= (1 << slice_bits)) return fail(DTC_EINVAL, "slice out of range");
+  DTC_HIP(hipSetDevice(ctx->device));
+  const int nsub = nl - k - slice_bits;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->prof) {
+    e0 = get_event(ctx);
+    e1 = get_event(ctx);
+    DTC_HIP(hipEventRecord(e0, ctx->stream));
+  }
+  DTC_HIP(dtc::launch_exchange_swap((double2*)state, nl, k, nsub, slice, ctx->stream));
+  if (ctx->prof) {
+    DTC_HIP(hipEventRecord(e1, ctx->stream));
+    // every off-diagonal piece read once and written once
+    const double moved = (double)((1 << k) * ((1 << k) - 1)) * (double)((int64_t)1 << nsub);
+    ctx->pending.push_back(Pending{DTC_KERNEL_EXCHANGE, e0, e1, 32.0 * moved});
   }
   return DTC_OK;
 }

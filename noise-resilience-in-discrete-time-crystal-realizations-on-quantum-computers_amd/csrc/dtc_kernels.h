@@ -212,4 +212,11 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx,
                             int batch, hipStream_t stream);
 
+// Virtual ranks' in-place all-to-all of one slice: 2^k shards of 2^nl
+// amplitudes, chunk = top k local bits, slice = the next nl - k - nsub bits;
+// piece (shard r, chunk c, slice) <-> piece (shard c, chunk r, slice), r != c.
+// Requires nsub >= 10 (1024 amplitudes per workgroup).
+hipError_t launch_exchange_swap(double2* state, int nl, int k, int nsub, int slice,
+                                hipStream_t stream);
+
 }  // namespace dtc

@@ -1640,4 +1640,50 @@ hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* id
   return hipGetLastError();
 }
 
+// In-place all-to-all of one slice over W = 2^k virtual shards held in one
+// buffer (the one-GPU stand-in for C5's xGMI exchange, sharded.py): piece
+// (r, c) = slice `slice` of chunk c of shard r trades places with piece
+// (c, r), r < c.  blockIdx.y = pair; each thread moves kSwapPerThread
+// amplitudes of both pieces, 16-B accesses 256 threads apart (1 KiB per wave
+// instruction, coalesced), streaming hints (every byte is touched once).
+static constexpr int kSwapPerThread = 4;
+
+__global__ __launch_bounds__(256) void exchange_swap_kernel(double2* __restrict__ state, int nl,
+                                                            int k, int nsub, int slice) {
+  int p = blockIdx.y, r = 0;
+  const int W = 1 << k;
+  while (p >= W - 1 - r) {
+    p -= W - 1 - r;
+    ++r;
+  }
+  const int c = r + 1 + p;
+  const int64_t off = ((int64_t)slice << nsub) + (int64_t)blockIdx.x * (256 * kSwapPerThread) +
+                      threadIdx.x;
+  d2v* a = (d2v*)(state + ((int64_t)r << nl) + ((int64_t)c << (nl - k)) + off);
+  d2v* b = (d2v*)(state + ((int64_t)c << nl) + ((int64_t)r << (nl - k)) + off);
+  d2v va[kSwapPerThread], vb[kSwapPerThread];
+#pragma unroll
+  for (int j = 0; j < kSwapPerThread; ++j) {
+    va[j] = __builtin_nontemporal_load(a + 256 * j);
+    vb[j] = __builtin_nontemporal_load(b + 256 * j);
+  }
+#pragma unroll
+  for (int j = 0; j < kSwapPerThread; ++j) {
+    __builtin_nontemporal_store(vb[j], a + 256 * j);
+    __builtin_nontemporal_store(va[j], b + 256 * j);
+  }
+}
+
+hipError_t launch_exchange_swap(double2* state, int nl, int k, int nsub, int slice,
+                                hipStream_t stream) {
+  // the grid covers each piece exactly: 2^nsub amplitudes, 1024 per workgroup
+  if (k < 1 || nsub < 10 || nsub + k > nl || nl > 40) return hipErrorInvalidValue;
+  const int pairs = ((1 << k) * ((1 << k) - 1)) / 2;
+  const int64_t blocks = ((int64_t)1 << nsub) / (256 * kSwapPerThread);
+  if (blocks > 0x7FFFFFFF || pairs > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(exchange_swap_kernel, dim3((unsigned)blocks, pairs), dim3(256), 0, stream,
+                     state, nl, k, nsub, slice);
+  return hipGetLastError();
+}
+
 }  // namespace dtc

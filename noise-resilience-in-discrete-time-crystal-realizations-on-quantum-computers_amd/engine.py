@@ -332,6 +332,19 @@ class DtcEngine:
             ctypes.c_int32(period), ctypes.c_uint64(pre_mask), ctypes.c_int32(chunk_bits),
             ctypes.c_int32(slice_bits), ctypes.c_int32(slice_), ctypes.c_void_p(state_ptr)))
 
+    def release_buffers(self):
+        """Free the engine's batch work buffers (dtc_release_buffers); the
+        next call re-allocates what it needs."""
+        _capi.check(self._lib.dtc_release_buffers(self._ctx))
+
+    def shard_exchange_slice(self, shard, slice_bits: int, slice_: int, state_ptr: int):
+        """Virtual ranks (every shard in ``state_ptr``): the all-to-all of slice
+        ``slice_`` in place -- piece (shard r, chunk c) <-> (shard c, chunk r) --
+        asynchronously on the engine stream (one launch)."""
+        _capi.check(self._lib.dtc_shard_exchange_slice(
+            self._ctx, ctypes.byref(shard), ctypes.c_int32(slice_bits), ctypes.c_int32(slice_),
+            ctypes.c_void_p(state_ptr)))
+
     def stream_handle(self) -> int:
         """The engine's hipStream_t (for torch.cuda.ExternalStream)."""
         h = ctypes.c_void_p()

@@ -183,13 +183,16 @@ class EngineStepper:
     def plan_groups(self, n_bits):
         return _capi.plan_groups(n_bits)
 
-    def alloc(self, layout: ShardLayout):
+    def alloc(self, layout: ShardLayout, n_buffers: int = 2):
         import torch
 
         n = layout.n_shards << layout.n_local
         dev = torch.device("cuda", torch.cuda.current_device())
-        return (torch.empty(n, dtype=torch.complex128, device=dev),
-                torch.empty(n, dtype=torch.complex128, device=dev))
+        return tuple(torch.empty(n, dtype=torch.complex128, device=dev)
+                     for _ in range(n_buffers))
+
+    def exchange_slice(self, layout: ShardLayout, slice_bits, slice_, buf):
+        self.engine.shard_exchange_slice(layout.to_c(), slice_bits, slice_, buf.data_ptr())
 
     def set_basis(self, spec, layout, seed, traj, buf):
         import torch
@@ -267,6 +270,23 @@ def sharded_forward(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0, t
 
 # ---- the pipelined sweep (C5 on the GPU node) -----------------------------------------
 
+def slice_p2p_plan(rank: int, W: int):
+    """The point-to-point transfers of one slice at rank ``rank`` of ``W``
+    (the real-rank exchange of sharded_forward_pipelined), in posting order:
+    ``[("isend" | "irecv", peer, chunk), ...]`` -- at step i = 1 .. W-1 send
+    chunk d = rank+i to rank d and receive chunk q = rank-i's piece from rank q
+    into chunk slot q.  Every peer appears once as a destination and once as a
+    source, so all W-1 xGMI links of a rank carry one transfer per slice; the
+    local chunk (c = rank) is a device copy, not listed.  Rank r's send to d
+    pairs with rank d's receive from r (same step i on both sides)."""
+    ops = []
+    for i in range(1, W):
+        d, q = (rank + i) % W, (rank - i) % W
+        ops.append(("isend", d, d))
+        ops.append(("irecv", q, q))
+    return ops
+
+
 class _SliceExchange:
     """All-to-all of one period as S slice transfers, each started as soon as
     its slice has been kicked.
@@ -275,37 +295,54 @@ class _SliceExchange:
     c), the next slice_bits number the slices of every chunk.  Step s sends
     slice s of every chunk to its rank and receives slice s of this rank's
     chunk from every rank -- all peers at once, so every xGMI link carries a
-    transfer (one ``batch_isend_irecv`` of 7 sends and 7 receives at 8 ranks;
-    the local slice is a device copy).  The transfers run on a side stream
-    that waits for the slice's kick (an event on the engine stream); the
-    engine stream waits for all of them before the fused pass.  Virtual ranks
-    (one process): slice s of every chunk of every shard is copied to its shard
-    on the side stream.  CPU tensors (gloo tests): the same transfers,
+    transfer (one ``batch_isend_irecv`` of 7 sends and 7 receives at 8 ranks,
+    ``slice_p2p_plan``; the local slice is a device copy).  The transfers run
+    on a side stream that waits for the slice's kick (an event on the engine
+    stream); the engine stream waits for all of them before the fused pass.
+    Virtual ranks (one process): slice s of every chunk of every shard is
+    copied to its shard on the side stream, or -- ``inplace`` -- swapped with
+    its partner piece in the same buffer on the engine stream
+    (``dtc_shard_exchange_slice``: no second state buffer, so an L=34 state
+    fits one GPU).  CPU tensors (gloo tests): the same transfers,
     synchronously."""
 
-    def __init__(self, stepper, W, S, rank, world, group):
+    def __init__(self, stepper, W, S, rank, world, group, inplace=False, slice_bits=0):
         import torch
 
         self.W, self.S, self.rank, self.world, self.group = W, S, rank, world, group
+        self.inplace, self.slice_bits = inplace, slice_bits
+        self.stepper = stepper
         self.cuda = hasattr(stepper, "stream")
         self.eng = stepper.stream() if self.cuda else None
-        self.side = torch.cuda.Stream() if self.cuda else None
+        self.side = torch.cuda.Stream() if (self.cuda and not inplace) else None
         self.works = []
-        self.t_events = []  # (start, end) per period, side stream
+        self.t_events = []  # (start, end) per period, side stream (engine stream in place)
 
-    def send(self, s, src, dst):
+    def _mark_start(self, s, stream):
+        import torch
+
+        if s == 0:
+            start = torch.cuda.Event(enable_timing=True)
+            start.record(stream)
+            self.t_events.append([start, None])
+
+    def send(self, s, src, dst, layout=None):
         import torch
         import torch.distributed as dist
 
         W, S = self.W, self.S
+        if self.inplace:
+            # one process holds every shard: swap piece (r, c) <-> (c, r) of
+            # slice s in place, ordered on the engine stream after its kick
+            if self.cuda:
+                self._mark_start(s, self.eng)
+            self.stepper.exchange_slice(layout, self.slice_bits, s, src)
+            return
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(self.eng)
             self.side.wait_event(ev)
-            if s == 0:
-                start = torch.cuda.Event(enable_timing=True)
-                start.record(self.side)
-                self.t_events.append([start, None])
+            self._mark_start(s, self.side)
             ctx = torch.cuda.stream(self.side)
         else:
             import contextlib
@@ -319,10 +356,13 @@ class _SliceExchange:
             r = self.rank
             dv[r, s].copy_(sv[r, s])
             ops = []
-            for i in range(1, W):
-                d, q = (r + i) % W, (r - i) % W
-                ops.append(dist.P2POp(dist.isend, torch.view_as_real(sv[d, s]), d, self.group))
-                ops.append(dist.P2POp(dist.irecv, torch.view_as_real(dv[q, s]), q, self.group))
+            for kind, peer, chunk in slice_p2p_plan(r, W):
+                if kind == "isend":
+                    ops.append(dist.P2POp(dist.isend, torch.view_as_real(sv[chunk, s]), peer,
+                                          self.group))
+                else:
+                    ops.append(dist.P2POp(dist.irecv, torch.view_as_real(dv[chunk, s]), peer,
+                                          self.group))
             reqs = dist.batch_isend_irecv(ops)
             if self.cuda:
                 self.works.extend(reqs)
@@ -334,6 +374,11 @@ class _SliceExchange:
         import torch
 
         if not self.cuda:
+            return
+        if self.inplace:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(self.eng)
+            self.t_events[-1][1] = end
             return
         with torch.cuda.stream(self.side):
             for w in self.works:
@@ -352,7 +397,8 @@ class _SliceExchange:
 
 def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0,
                               traj: int = 0, seed: int = 0x5EED0001, rank: int = 0,
-                              world: int = 1, group=None, buffers=None, stats=None):
+                              world: int = 1, group=None, buffers=None, stats=None,
+                              inplace: bool = False):
     """``sharded_forward`` with the exchange overlapped and no host round trip
     per period (the C5 schedule on the GPU node).
 
@@ -367,8 +413,16 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     array; the host reads them once at the end and joins the ranks with one
     all-reduce.  Same results as ``sharded_forward``.
 
+    ``inplace`` (virtual ranks only): one state buffer; each slice's exchange
+    swaps the pieces (r, c) and (c, r) in place (``stepper.exchange_slice``,
+    dtc_shard_exchange_slice) on the engine stream and the fused pass runs in
+    place -- the layout and kernels of the 8-GPU run at a quarter of the memory
+    of two buffers (an L=34 state is 256 GiB).  ``buffers`` is then ``(A,)``
+    or ``(A, None)``.
+
     ``stats`` (dict, optional) receives the per-period exchange windows (ms,
-    side-stream events) on the GPU."""
+    side-stream events; engine-stream events in place) and the per-period wall
+    of the engine stream (``period_ms``) on the GPU."""
     import torch
 
     L, T = spec.L, spec.T
@@ -377,7 +431,16 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
         raise ValueError("world must be 1 (virtual ranks) or 2^n_global")
     n_sh = W // world
     lay = initial_layout(L, n_global, rank * n_sh, n_sh)
-    A, Bf = buffers if buffers is not None else stepper.alloc(lay)
+    if inplace and world != 1:
+        raise ValueError("the in-place exchange needs every shard in one process (world 1)")
+    if buffers is not None:
+        A, Bf = (tuple(buffers) + (None,))[:2]
+    elif inplace:
+        A, Bf = stepper.alloc(lay, n_buffers=1)[0], None
+    else:
+        A, Bf = stepper.alloc(lay)
+    if inplace:
+        Bf = A
     nl, top, allb = lay.n_local, lay.top_mask, lay.local_mask
     groups = stepper.plan_groups(nl)
     main = next(g for g in groups if (g >> (nl - 1)) & 1)
@@ -392,14 +455,25 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     slice_bits = max(0, min(3, nl - n_global - 1 - pre_top, nl - n_global - tile))
     chunked = nl - n_global - slice_bits >= tile
     S = 1 << slice_bits if chunked else 1
+    if inplace and not chunked:
+        raise ValueError("the in-place exchange needs chunks of at least one tile")
     P = T - 1 + spec.t_offset
     obs = stepper.obs_buffer(P + 1, n_sh, 1 + nl)
     layouts = [lay]
-    xch = _SliceExchange(stepper, W, S, rank, world, group)
+    xch = _SliceExchange(stepper, W, S, rank, world, group, inplace=inplace,
+                         slice_bits=slice_bits if chunked else 0)
+    marks = [] if xch.cuda else None  # engine-stream events, one per period boundary
+
+    def mark():
+        if marks is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(xch.eng)
+            marks.append(e)
 
     stepper.set_basis(spec, lay, seed, traj, A)
     stepper.step_async(spec, lay, seed, traj, inst, 1, 0, False, 0, A, A, obs[0])
     kicked = 0
+    mark()
     for p in range(1, P + 1):
         pre = allb & ~kicked
         if pre & post_bits or not chunked:
@@ -412,13 +486,14 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
             if pre:
                 stepper.kick_slice(spec, lay, seed, traj, p, pre, n_global, slice_bits if chunked
                                    else 0, sl, A)
-            xch.send(sl, A, Bf)
+            xch.send(sl, A, Bf, lay)
         xch.finish()
         lay = lay.exchanged()
         post = post_bits if p < P else 0
         stepper.step_async(spec, lay, seed, traj, inst, p, top, True, post, Bf, A, obs[p])
         layouts.append(lay)
         kicked = post
+        mark()
     stepper.synchronize()
     o = obs.cpu().numpy() if hasattr(obs, "cpu") else np.asarray(obs)
     z = np.stack([z_from_obs(layouts[p], o[p]) for p in range(P + 1)])
@@ -432,5 +507,7 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
             norm[t], zs[t] = z[p, 0], z[p, 1:]
     if stats is not None:
         stats["exchange_ms"] = xch.exchange_ms() if xch.cuda else []
+        stats["period_ms"] = ([a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:])]
+                              if marks else [])
     fac = (1.0 - spec.p) ** N_ANCILLA_NOISY_GATES
     return {"zsite": zs, "norm": norm, "fwd": fac * zinit * zs[:, spec.probe_site]}

@@ -12,6 +12,27 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
+LIB_PATH_V3 = os.path.join(_HERE, "liboracle_v3.so")  # -march=x86-64-v3 build (Makefile)
+_V3_FLAGS = {"avx", "avx2", "bmi1", "bmi2", "f16c", "fma", "movbe", "abm"}
+
+
+def _host_has_v3() -> bool:
+    """The x86-64-v3 feature set in /proc/cpuinfo (else the portable build)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    return _V3_FLAGS <= set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return False
+
+
+def lib_path() -> str:
+    """The build this host runs: the x86-64-v3 one when present and supported."""
+    if os.path.exists(LIB_PATH_V3) and _host_has_v3():
+        return LIB_PATH_V3
+    return LIB_PATH
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -44,9 +65,10 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"oracle not built: {LIB_PATH} (run `make`)")
-        _lib = ctypes.CDLL(LIB_PATH)
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: {path} (run `make`)")
+        _lib = ctypes.CDLL(path)
         _lib.orc_autocorr.argtypes = [ctypes.POINTER(OrcProblem), ctypes.POINTER(OrcNoise),
                                       ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, _dp, _dp,
                                       _dp, ctypes.c_int32]

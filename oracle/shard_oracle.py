@@ -41,11 +41,11 @@ class NumpyShardStepper:
             return self._groups(n_bits)
         return [(1 << n_bits) - 1]
 
-    def alloc(self, layout):
+    def alloc(self, layout, n_buffers=2):
         import torch
 
         n = layout.n_shards << layout.n_local
-        return (torch.zeros(n, dtype=torch.complex128), torch.zeros(n, dtype=torch.complex128))
+        return tuple(torch.zeros(n, dtype=torch.complex128) for _ in range(n_buffers))
 
     # -- helpers --------------------------------------------------------
     @staticmethod
@@ -140,6 +140,19 @@ class NumpyShardStepper:
             if (pre >> q) & 1:
                 self._apply(sub, nsub, q, self._kick(spec, period, layout.site_of[q], seed, traj))
         psi[:, slice_, :] = sub
+
+    def exchange_slice(self, layout, slice_bits, slice_, buf):
+        """dtc_shard_exchange_slice: every shard in ``buf``; piece (shard r,
+        chunk c, slice) <-> (shard c, chunk r, slice), in place."""
+        W = 1 << layout.n_global
+        if layout.n_shards != W or layout.first_rank != 0:
+            raise ValueError("the in-place exchange needs every shard in this buffer")
+        v = buf.numpy().reshape(W, W, 1 << slice_bits, -1)
+        for r in range(W):
+            for c in range(r + 1, W):
+                tmp = v[r, c, slice_].copy()
+                v[r, c, slice_] = v[c, r, slice_]
+                v[c, r, slice_] = tmp
 
     def step_async(self, spec, layout, seed, traj, inst, period, pre, diag, post, src, dst,
                    obs_out):

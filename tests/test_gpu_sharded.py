@@ -106,3 +106,49 @@ def test_l32_eight_virtual_ranks_pipelined(pkg, engine, stepper):
     assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
     assert np.abs(got["zsite"][1] - np.cos(np.pi * 0.97)).max() < 1e-12
     assert np.abs(got["norm"] - 1.0).max() < 1e-10
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (22, 3, 5, 0.05, "neel", "x", 0),
+    (26, 2, 4, 0.1, "vacuum", "circular_left", 0),
+    (25, 3, 4, 0.05, "neel", "xy", 1),
+])
+def test_pipelined_inplace_virtual_shards_match_engine(pkg, engine, stepper, L, k, T, p, state,
+                                                       pol, toff):
+    """One state buffer: every slice's exchange is the in-place piece swap
+    (dtc_shard_exchange_slice, exchange_swap_kernel) on the engine stream and
+    the fused pass runs in place -- the L=34 path at sizes the whole-state
+    engine also runs, per trajectory to 1e-10."""
+    rng = np.random.default_rng(L * 13 + k)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    one = dataclasses.replace(spec, hs=hs[1:2], phis=phis[1:2])
+    for traj in (0, 5):
+        got = pkg.sharded.sharded_forward_pipelined(stepper, spec, k, inst=1, traj=traj, seed=77,
+                                                    inplace=True)
+        ref = engine.autocorr(one, 1, seed=77, traj_offset=traj, want_echo=False,
+                              want_zsite=True)
+        assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+        assert np.abs(got["norm"] - 1.0).max() < 1e-10
+
+
+def test_exchange_slice_is_the_all_to_all(pkg, engine, stepper):
+    """The in-place swap of every slice equals the two-buffer virtual exchange
+    (dst[r][c] = src[c][r]) bit for bit, and twice is the identity."""
+    import torch
+
+    lay = pkg.sharded.initial_layout(24, 3, 0, 8)
+    x = torch.randn(1 << 24, dtype=torch.complex128, device="cuda")
+    ref = torch.empty_like(x)
+    pkg.sharded.virtual_exchange(x, ref, 8)
+    y = x.clone()
+    torch.cuda.synchronize()  # the swaps run on the engine's stream
+    for s in range(4):
+        stepper.exchange_slice(lay, 2, s, y)
+    engine.synchronize()
+    assert torch.equal(y, ref)
+    for s in range(4):
+        stepper.exchange_slice(lay, 2, s, y)
+    engine.synchronize()
+    assert torch.equal(y, x)

@@ -152,3 +152,127 @@ def test_gloo_ranks_match_oracle(pkg, k, pipelined, L):
     one = dataclasses.replace(spec, hs=spec.hs[:1], phis=spec.phis[:1])
     ref = c_oracle.autocorr(one, 1, seed=5, traj_offset=2, want_zsite=True, want_echo=False)
     assert np.abs(got - ref["zsite"][0, 0]).max() < 1e-12
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (7, 2, 6, 0.1, "neel", "circular_left", 0),
+    (9, 3, 5, 0.05, "neel", "xy", 1),
+    (10, 2, 4, 0.1, "vacuum", "x", 0),    # 4 slices per chunk
+    (11, 1, 4, 0.05, "neel", "y", 0),     # 8 slices per chunk
+])
+@pytest.mark.parametrize("groups", [None, _halves])
+def test_pipelined_inplace_virtual_ranks_match_oracle(pkg, L, k, T, p, state, pol, toff, groups):
+    """The one-buffer variant (inplace=True: each slice's exchange swaps the
+    pieces (r, c) <-> (c, r) in place, dtc_shard_exchange_slice's semantics)
+    gives the whole-state oracle's per-site <Z_i(t)> -- the path that runs
+    C5's L=34 layout on one GPU."""
+    import dataclasses
+    spec = _spec(pkg, L, T, p, state, pol, toff)
+    for traj in (0, 3):
+        got = pkg.sharded.sharded_forward_pipelined(NumpyShardStepper(groups), spec, k, inst=1,
+                                                    traj=traj, seed=99, inplace=True)
+        one = dataclasses.replace(spec, hs=spec.hs[1:2], phis=spec.phis[1:2])
+        ref = c_oracle.autocorr(one, 1, seed=99, traj_offset=traj, want_zsite=True,
+                                want_echo=False)
+        assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < 1e-12
+        assert np.abs(got["norm"] - 1.0).max() < 1e-12
+
+
+def test_inplace_exchange_is_the_all_to_all(pkg):
+    """Swapping every slice in place equals the two-buffer virtual exchange
+    (dst[r][c] = src[c][r]), and a second exchange restores the state."""
+    import torch
+
+    lay = pkg.sharded.initial_layout(9, 2, 0, 4)
+    x = torch.randn(4 << 7, dtype=torch.complex128)
+    ref = torch.empty_like(x)
+    pkg.sharded.virtual_exchange(x, ref, 4)
+    y = x.clone()
+    st = NumpyShardStepper()
+    for s in range(4):
+        st.exchange_slice(lay, 2, s, y)
+    assert torch.equal(y, ref)
+    for s in range(4):
+        st.exchange_slice(lay, 2, s, y)
+    assert torch.equal(y, x)
+    with pytest.raises(ValueError):
+        pkg.sharded.sharded_forward_pipelined(st, _spec(pkg, 9, 3), 2, world=4, inplace=True)
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_slice_p2p_plan_pairs_every_send_with_a_receive(pkg, W):
+    """The real-rank op list (sharded.slice_p2p_plan): at every step each
+    rank sends to one peer and receives from one, every peer exactly once per
+    slice, and rank r's send at step i is the receive its peer posts at step
+    i (so the batched point-to-point ops of the 8-GPU exchange match up)."""
+    plans = {r: pkg.sharded.slice_p2p_plan(r, W) for r in range(W)}
+    for r, ops in plans.items():
+        assert len(ops) == 2 * (W - 1)
+        sends = [(peer, chunk) for kind, peer, chunk in ops if kind == "isend"]
+        recvs = [(peer, chunk) for kind, peer, chunk in ops if kind == "irecv"]
+        assert sorted(p for p, _ in sends) == sorted(set(range(W)) - {r})
+        assert sorted(p for p, _ in recvs) == sorted(set(range(W)) - {r})
+        assert all(p == c for p, c in sends)      # chunk d goes to rank d
+        assert all(p == c for p, c in recvs)      # rank q's piece lands in slot q
+        for i, ((_, d, _), (_, q, _)) in enumerate(zip(ops[0::2], ops[1::2])):
+            partner = plans[d][2 * i + 1]          # d's receive at the same step
+            assert partner[:2] == ("irecv", r)
+            assert plans[q][2 * i][:2] == ("isend", r)
+
+
+def _exchange_worker(rank, world, port, S, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from __graft_entry__ import load_package
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = load_package()
+    n = 16  # amplitudes per (chunk, slice) piece
+    # piece (chunk c, slice s) of rank r holds the value r + 100 c + 10000 s + j / 64
+    j = torch.arange(n, dtype=torch.float64) / 64
+    src = torch.zeros(world * S * n, dtype=torch.complex128)
+    sv = src.view(world, S, n)
+    for c in range(world):
+        for s in range(S):
+            sv[c, s] = (rank + 100 * c + 10000 * s + j).to(torch.complex128)
+    dst = torch.full_like(src, -1.0)
+    xch = pkg.sharded._SliceExchange(NumpyShardStepper(), world, S, rank, world, None)
+    for s in range(S):
+        xch.send(s, src, dst)
+    xch.finish()
+    dv = dst.view(world, S, n)
+    ok = True
+    for qq in range(world):
+        for s in range(S):
+            want = (qq + 100 * rank + 10000 * s + j).to(torch.complex128)
+            ok &= bool(torch.equal(dv[qq, s], want))
+    flag = torch.tensor([1.0 if ok else 0.0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put(float(flag.item()))
+    dist.destroy_process_group()
+
+
+def test_gloo_world8_slice_exchange_delivers_every_piece(pkg):
+    """World 8 (the C5 rank count) over gloo: the batched point-to-point ops
+    built from slice_p2p_plan deliver slice s of chunk r of every rank q into
+    slot q of rank r, for every slice -- the all-to-all, piece by piece."""
+    world, S = 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, S, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=180)
+    for pr in procs:
+        pr.join(timeout=180)
+        assert pr.exitcode == 0
+    assert got == 1.0
