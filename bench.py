@@ -46,12 +46,13 @@ PKG = "noise-resilience-in-discrete-time-crystal-realizations-on-quantum-compute
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-HBM_MEASURED_GBS = 6290.0    # float4 copy measured (same table)
-BOX_COPY_GBS = 5715.0        # best copy-kernel read+write stream measured on this part (in place,
-                             # 4 x 16 B per lane; tools/hbm_ceiling.hip, profiles/r2d_hbm_ceiling.txt:
-                             # read alone 7.0-7.3 TB/s, write alone 5.2 TB/s)
-BEST_RW_PASS_GBS = 6080.0    # best read+write rate any pass kernel reached on this part: a
-                             # 12-site kick-only pass over L=28 states (profiles/r2ak_state_size.txt)
+HBM_MEASURED_GBS = 6290.0    # the guide's measured float4 copy (same table)
+# The best read+write stream measured on this part (tools/hbm_ceiling2.hip,
+# profiles/r3b_hbm_ceiling2.txt): an in-place sweep with ONE 16-B amplitude per
+# lane and nontemporal loads/stores, 6.59 TB/s (copy 6.53).  The same sweep with
+# 4 / 16 amplitudes per lane (16 / 64 KiB per workgroup, the pass kernels' tile)
+# reaches 5.66 / 5.4 TB/s (r3b, r2d).
+BEST_RW_STREAM_GBS = 6586.0
 METRIC = "Floquet-periods×instances/sec at L=20; RZZ-kernel HBM GB/s vs peak"
 
 
@@ -104,9 +105,11 @@ def cpu_baseline(spec, n_traj, T_sample, threads=None, t_offset=0):
     }
 
 
-def read_traffic(bytes_per_launch, suffix="_pmc.json"):
+def read_traffic(bytes_per_launch, suffix="_pmc.json", batch=None):
     """HBM bytes per launch of the RZZ kernel from the latest committed PMC
-    summary named *<suffix> (tools/pmc_summary.py output), or None."""
+    summary named *<suffix> (tools/pmc_summary.py output: rocprofv3 FETCH_SIZE
+    and WRITE_SIZE passes of this same bench config), or (None, None).  With
+    ``batch``, only a summary taken at that batch counts (no rescaling)."""
     import re
 
     def tag_order(path):
@@ -115,10 +118,16 @@ def read_traffic(bytes_per_launch, suffix="_pmc.json"):
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, path)
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)), key=tag_order)
-    if not files:
+    d = None
+    for path in reversed(files):
+        with open(path) as f:
+            cand = json.load(f)
+        if batch is None or cand.get("batch") == batch:
+            d = cand
+            files = [path]
+            break
+    if d is None:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
     k = d.get("lo_pass")
     if not k or not k.get("hbm_bytes_per_launch"):
         return None, None
@@ -474,11 +483,22 @@ def main(argv=None):
     value = total_units / elapsed
     lo = stats[0]
     hi = stats[1]
-    launch_bytes = 32.0 * (1 << max(args.L, 12)) * B
+    # algorithmic bytes per launch as the engine booked them (32 B per amplitude
+    # for a read+store pass; 16 B for the first pass, which forms the basis
+    # states in registers and only stores, and for the measure-only passes)
+    launch_bytes = lo["bytes"] / max(1, lo["launches"])
+    hi_bytes = hi["bytes"] / max(1, hi["launches"])
     avg_lo = lo["total_ms"] / max(1, lo["launches"]) / 1e3
     avg_hi = hi["total_ms"] / max(1, hi["launches"]) / 1e3
     achieved = launch_bytes / avg_lo / 1e9 if lo["launches"] else 0.0
-    traffic, traffic_src = read_traffic(launch_bytes)
+    traffic, traffic_src = read_traffic(launch_bytes, "_pmc_c3.json" if c3 else "_pmc.json",
+                                        batch=B)
+    # what the engine executed (the value credits whole period applications;
+    # the schedule runs fewer, larger passes: K-D-K passes that each advance a
+    # period, light-cone passes that replace the last 2-4 of an echo chain)
+    n_launch = {k: stats[k]["launches"] / args.steps for k in (0, 1, 4)}
+    state_passes = sum(stats[k]["launches"] for k in (0, 1, 4)) * B
+    hbm_bytes_kernels = sum(stats[k]["bytes"] for k in (0, 1, 4, 5))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
@@ -541,8 +561,7 @@ def main(argv=None):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "frac_of_measured_copy": achieved / HBM_MEASURED_GBS,
-            "frac_of_box_copy": achieved / BOX_COPY_GBS,
-            "frac_of_best_rw_pass": achieved / BEST_RW_PASS_GBS,
+            "frac_of_best_rw_stream": achieved / BEST_RW_STREAM_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": launch_bytes,
@@ -555,7 +574,10 @@ def main(argv=None):
             "kdk_pass": {"launches": lo["launches"], "avg_ms": avg_lo * 1e3,
                         "GBps": launch_bytes / avg_lo / 1e9 if lo["launches"] else None},
             "kick_pass": {"launches": hi["launches"], "avg_ms": avg_hi * 1e3,
-                        "GBps": launch_bytes / avg_hi / 1e9 if hi["launches"] else None},
+                          "bytes_per_launch": hi_bytes,
+                          "GBps": hi_bytes / avg_hi / 1e9 if hi["launches"] else None,
+                          "note": "first pass of a sweep: basis states formed in registers, "
+                                  "store only (16 B/amp)"},
             "final_pass": {"launches": stats[4]["launches"], "avg_ms":
                            stats[4]["total_ms"] / max(1, stats[4]["launches"]),
                            "GBps": stats[4]["bytes"] / (stats[4]["total_ms"] / 1e3) / 1e9
@@ -563,6 +585,18 @@ def main(argv=None):
                            "note": "last pass of each echo chain: measure only, no store (16 B/amp)"},
             "reduce": {"launches": stats[2]["launches"], "total_ms": stats[2]["total_ms"]},
             "kernel_time_frac": sum(stats[k]["total_ms"] for k in stats) / (elapsed * 1e3),
+        },
+        "executed": {
+            "note": ("value counts period applications of the full forward+echo sweep "
+                     "(output-equivalent: the same per-trajectory results, oracle 1e-10); "
+                     "the engine executes them as the passes below"),
+            "launches_per_step": {"kdk_pass": n_launch[0], "kick_pass": n_launch[1],
+                                  "lightcone_final_pass": n_launch[4]},
+            "state_passes_per_step": state_passes / args.steps,
+            "executed_state_passes_per_s": world * state_passes / elapsed,
+            "period_applications_per_state_pass": (total_units / world) / max(1, state_passes),
+            "algorithmic_hbm_bytes_per_step": hbm_bytes_kernels / args.steps,
+            "algorithmic_hbm_GBps_over_timed_region": hbm_bytes_kernels / elapsed / 1e9,
         },
         "reference_equivalent": {
             "note": ("the reference runs one 1024-shot circuit per t (fwd and echo): "
@@ -663,7 +697,8 @@ def main_c4(args):
                    "parallelism": f"instance-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": "dtc_kdk_pass (+ dtc_kick_pass, 2 passes/period)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "frac_of_box_copy": achieved / BOX_COPY_GBS,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "frac_of_best_rw_stream": achieved / BEST_RW_STREAM_GBS,
                      "traffic": None, "algorithmic_bytes_per_launch": launch_bytes,
                      "avg_launch_ms": avg_lo * 1e3, "launches": lo_s["launches"]},
         "kernels": {"kdk_pass": {"launches": lo_s["launches"], "avg_ms": avg_lo * 1e3},
@@ -908,7 +943,7 @@ def _pass_kernels(stats, elapsed):
     achieved = lo_b / avg_lo / 1e9 if lo_s["launches"] else 0.0
     roof = {"bound": "hbm", "kernel": "dtc_kdk_pass", "achieved": achieved,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "frac_of_box_copy": achieved / BOX_COPY_GBS, "traffic": None,
+            "frac_of_best_rw_stream": achieved / BEST_RW_STREAM_GBS, "traffic": None,
             "algorithmic_bytes_per_launch": lo_b, "avg_launch_ms": avg_lo * 1e3,
             "launches": lo_s["launches"]}
     kern = {"kdk_pass": {"launches": lo_s["launches"], "avg_ms": avg_lo * 1e3},
@@ -961,7 +996,7 @@ def main_energy(args):
     roof["kernel"] = ("dtc_kdk_pass (one forward period; Z, ZZ after the diagonal and X before "
                       "each site's kick measured in flight)")
     roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"],
-                                                           "_pmc_energy.json")
+                                                           "_pmc_energy.json", batch=B)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_energy(spec, args.cpu_traj or 2 * _host_threads(),
@@ -1039,8 +1074,9 @@ def main_ctrl(args):
     per_loop = shots * sum(2 * (t + 1) for t in range(T))
     n_loops = world * args.steps
     roof, kern = _pass_kernels(stats, elapsed)
-    # the same kernel (probe measurement) as C2: its PMC ratio, scaled
-    roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"])
+    # its own PMC passes (tools/pmc_traffic.sh with BENCH_ARGS="--config ctrl"), if any
+    roof["traffic"], roof["traffic_source"] = read_traffic(roof["algorithmic_bytes_per_launch"],
+                                                           "_pmc_ctrl.json", batch=shots)
     cpu = None
     # (the optimisation loop's evaluation count is data-dependent: no fixed CPU work unit)
     if world == 1 and not args.no_cpu_baseline and not args.ctrl_opt:

@@ -3,8 +3,11 @@ per-launch HBM byte counts bench.py reports as roofline.traffic.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes
 of 16-B-per-lane coalesced streaming reads -> x2; WRITE_SIZE is exact for
-16-B-per-lane streaming stores.  Units: KiB.
-usage: python tools/pmc_summary.py <prof_dir> <out.json> <batch> <L>
+16-B-per-lane streaming stores.  Units: KiB.  Algorithmic bytes per launch:
+32 B per amplitude for a pass that reads and stores its states, 16 B for one
+that only stores (the basis-synthesising first pass: no fetch) or only reads
+(the measure-only light-cone / final passes).
+usage: python tools/pmc_summary.py <prof_dir> <out.json> <batch> <L> [bench args]
 """
 import json
 import sys
@@ -12,23 +15,33 @@ import sys
 import pandas as pd
 
 
-def main(prof, out, batch, L):
+def main(prof, out, batch, L, bench_args=""):
     fe = pd.read_csv(f"{prof}/fetch_counter_collection.csv")
     wr = pd.read_csv(f"{prof}/write_counter_collection.csv")
-    res = {"source": prof, "batch": batch, "L": L,
+    res = {"source": prof, "batch": batch, "L": L, "bench_args": bench_args,
            "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 FETCH_SIZE halving"}
-    alg = 32.0 * (1 << max(L, 12)) * batch
-    for kname, key in (("dtc_kdk_pass", "lo_pass"), ("dtc_kick_pass", "hi_pass")):
-        f = fe[fe.Kernel_Name.str.contains(kname)]["Counter_Value"].mean() * 1024
-        w = wr[wr.Kernel_Name.str.contains(kname)]["Counter_Value"].mean() * 1024
-        res[key] = {"kernel": kname, "fetch_bytes_raw": f, "write_bytes": w,
-                    "hbm_bytes_per_launch": 2 * f + w,
+    amps = float(1 << max(L, 12)) * batch
+    for kname, key in (("dtc_kdk_pass", "lo_pass"), ("dtc_kick_pass", "hi_pass"),
+                       ("dtc_lc_final", "lightcone_pass")):
+        fsel = fe[fe.Kernel_Name.str.contains(kname)]["Counter_Value"]
+        wsel = wr[wr.Kernel_Name.str.contains(kname)]["Counter_Value"]
+        if not len(fsel) or not len(wsel):
+            continue
+        f = fsel.mean() * 1024
+        w = wsel.mean() * 1024
+        hbm = 2 * f + w
+        reads = 2 * f > 0.01 * hbm
+        writes = w > 0.01 * hbm
+        alg = (16.0 * (int(reads) + int(writes))) * amps
+        res[key] = {"kernel": kname, "launches": int(len(fsel)), "fetch_bytes_raw": f,
+                    "write_bytes": w, "hbm_bytes_per_launch": hbm,
                     "algorithmic_bytes_per_launch": alg,
-                    "ratio_to_algorithmic": (2 * f + w) / alg}
+                    "ratio_to_algorithmic": hbm / alg}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]),
+         sys.argv[5] if len(sys.argv) > 5 else "")
