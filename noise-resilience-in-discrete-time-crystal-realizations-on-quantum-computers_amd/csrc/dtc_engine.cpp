@@ -89,6 +89,18 @@ struct dtc_ctx {
   int prefix_n_traj = 0, prefix_device = 0;
   uint64_t prefix_hash = 0;
   bool prof = false;
+  // options fixed at dtc_open (environment read once there; development A/B
+  // switches, documented in DESIGN.md): batch state layout, light-cone pass
+  // variant, the basis-synthesising first pass, the light-cone merge, batch
+  // memory budget, verbose batch report
+  int octet_bits = 6;        // DTC_OCTET_BITS (0 = contiguous states)
+  int lc_split = 1;          // DTC_LC_SPLIT
+  int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
+  bool basis_synth = true;   // DTC_NO_BASIS_SYNTH
+  bool lightcone = true;     // DTC_NO_LIGHTCONE
+  double batch_bytes = 0.0;  // DTC_BATCH_BYTES (0 = automatic)
+  bool verbose = false;      // DTC_VERBOSE
+  int prefix_octet = 0;      // layout the prefix states were built in
   int64_t st_n[DTC_KERNEL_KINDS] = {};
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
@@ -269,6 +281,7 @@ struct RunCfg {
   int noisy;
   uint32_t thr1, thr2, thr3;
   const int* site_of = nullptr;  // device: physical bit -> logical site (shards)
+  int octet_bits = 0;            // batch state layout (dtc_kernels.h state_base)
   // sharded state: the tables live in ctx->shard_cache / shard_kick, and a
   // chunk pass covers the low L_eff_override bits of states stride_override apart
   const double2* diag_tab = nullptr;
@@ -360,6 +373,9 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.diag_stride = rc.pl.diag_stride;
   A.probe = rc.prob->probe_site;
   A.partial = (double*)ctx->partial.p;
+  A.octet_bits = rc.octet_bits;
+  A.lc_split = ctx->lc_split;
+  A.lc_tpb = ctx->lc_tpb;
 #ifdef DTC_PHASE_TIMING
   if (const char* e = std::getenv("DTC_DBG_PTR")) A.dbg_ts = (uint64_t*)std::strtoull(e, nullptr, 0);
 #endif
@@ -611,15 +627,25 @@ int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
 // its schedule: a first pass that only kicks forms them in registers (no
 // zero-fill of F, no read of it); any other first pass reads F, filled here.
 template <class LaunchT>
-int basis_source(dtc_ctx* ctx, std::vector<LaunchT>& sched, double2* F, int64_t len, int nb) {
-  if (!sched.empty() && pass_shape(sched[0].ps) == dtc::kShapeK &&
-      std::getenv("DTC_NO_BASIS_SYNTH") == nullptr) {
+int basis_source(dtc_ctx* ctx, std::vector<LaunchT>& sched, double2* F, int64_t len, int nb,
+                 int octet_bits) {
+  if (!sched.empty() && pass_shape(sched[0].ps) == dtc::kShapeK && ctx->basis_synth) {
     sched[0].basis = (const int64_t*)ctx->basis.p;
     return DTC_OK;
   }
-  DTC_HIP(hipMemsetAsync(F, 0, (size_t)nb * len * 16, ctx->stream));
-  DTC_HIP(dtc::launch_set_basis(F, len, (const int64_t*)ctx->basis.p, nb, ctx->stream));
+  DTC_HIP(hipMemsetAsync(F, 0, (size_t)dtc::octet_padded(nb, octet_bits) * len * 16, ctx->stream));
+  DTC_HIP(dtc::launch_set_basis(F, len, (const int64_t*)ctx->basis.p, nb, ctx->stream, octet_bits));
   return DTC_OK;
+}
+
+// Batch size and state layout of a batched run: B states per launch within
+// the memory budget (per_state bytes each), the octet layout (dtc_kernels.h)
+// when a batch holds at least one octet; then B is a multiple of 8 unless one
+// batch takes every state.
+void batch_layout(const dtc_ctx* ctx, int64_t S, int64_t& B, int& octet) {
+  B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
+  octet = (ctx->octet_bits > 0 && B >= 8) ? ctx->octet_bits : 0;
+  if (octet && B < S) B &= ~(int64_t)7;
 }
 
 // Matrix family of each kick-table row: RX if every sub-gate is
@@ -954,6 +980,14 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   DTC_HIP(hipSetDevice(device));
   dtc_ctx* c = new dtc_ctx();
   c->device = device;
+  if (const char* e = std::getenv("DTC_OCTET_BITS")) c->octet_bits = std::atoi(e);
+  if (c->octet_bits != 0 && (c->octet_bits < 4 || c->octet_bits > 12)) c->octet_bits = 6;
+  if (const char* e = std::getenv("DTC_LC_SPLIT")) c->lc_split = e[0] != '0';
+  if (const char* e = std::getenv("DTC_LC_TPB")) c->lc_tpb = std::atoi(e);
+  c->basis_synth = std::getenv("DTC_NO_BASIS_SYNTH") == nullptr;
+  c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
+  if (const char* e = std::getenv("DTC_BATCH_BYTES")) c->batch_bytes = std::atof(e);
+  c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(DTC_EHIP, "hipStreamCreate failed");
@@ -1195,13 +1229,23 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     double budget = per_state >= (double)(256ull << 20)
                         ? 0.7 * (double)free_b
                         : std::min(0.6 * (double)free_b, 64.0 * (1ull << 30));
-    if (const char* env = std::getenv("DTC_BATCH_BYTES")) budget = std::atof(env);
+    if (ctx->batch_bytes > 0) budget = ctx->batch_bytes;
     B = (int64_t)(budget / per_state);
     B = std::max<int64_t>(1, std::min<int64_t>(B, 4096));
   }
-  B = std::min<int64_t>(B, S);
-  B = std::min<int64_t>(B, 65535);
-  if (std::getenv("DTC_VERBOSE")) {
+  int octet = 0;
+  batch_layout(ctx, S, B, octet);
+  if (use_prefix) {
+    // the prefix's states are in the layout they were built in
+    octet = ctx->prefix_octet;
+    if (octet && B < S) {
+      B &= ~(int64_t)7;
+      if (B < 8) return fail(DTC_EINVAL, "batch too small for the prefix's octet layout");
+    }
+  }
+  rc.octet_bits = octet;
+  const int64_t Bp = dtc::octet_padded(B, octet);
+  if (ctx->verbose) {
     size_t fr = 0, to = 0;
     (void)hipMemGetInfo(&fr, &to);
     std::fprintf(stderr, "[dtc] L=%d states=%lld batch=%lld state=%.3f GiB free=%.1f/%.1f GiB\n",
@@ -1209,8 +1253,8 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                  to / 1073741824.0);
   }
 
-  DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
-  if (want_e) DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));
+  DTC_TRY(ensure(ctx->F, (size_t)(Bp * pl.len * 16)));
+  if (want_e) DTC_TRY(ensure(ctx->E, (size_t)(Bp * pl.len * 16)));
   const int max_obs = std::max(n_obs_f, 2);
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * max_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_obs_f * sizeof(double)));
@@ -1230,6 +1274,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     double2* F = (double2*)ctx->F.p;
     double2* E = (double2*)ctx->E.p;
     // the first forward pass reads the prefix states (or the basis states in F)
+    // (bs is a multiple of 8 in the octet layout: the batch starts an octet)
     const double2* F0 = use_prefix ? (const double2*)ctx->prefix.p + (size_t)bs * pl.len : F;
     if (!use_prefix) {
       DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
@@ -1242,7 +1287,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                              ctx->stream));
 
     // DTC_NO_LIGHTCONE=1: keep the chains' last two passes (development A/B)
-    const bool lc_enabled = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
+    const bool lc_enabled = ctx->lightcone;
     // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
     // and branch the echo at t off F.  The whole batch schedule is built first.
     std::vector<Launch> sched;
@@ -1304,7 +1349,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         sched.back().no_store = 1;
       }
     }
-    if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
+    if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
@@ -1366,11 +1411,16 @@ int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   DTC_TRY(upload_tables(ctx, pr, pl));
   const int64_t S = (int64_t)pr->n_inst * n_traj;
   ctx->prefix_periods = -1;
-  DTC_TRY(ensure(ctx->prefix, (size_t)S * pl.len * 16));
+  // batches of up to 4096 states (multiples of 8): the octet layout whenever
+  // there is an octet; autocorr_prefixed reads them in this layout
+  int64_t B = 4096;
+  int octet = 0;
+  batch_layout(ctx, S, B, octet);
+  rc.octet_bits = octet;
+  DTC_TRY(ensure(ctx->prefix, (size_t)dtc::octet_padded(S, octet) * pl.len * 16));
   ctx->prefix_masks.resize(S);
   for (int64_t g = 0; g < S; ++g)
     ctx->prefix_masks[g] = (int64_t)init_state_mask(rc, (uint64_t)(traj_offset + g % n_traj));
-  const int64_t B = std::min<int64_t>(S, 4096);
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
   for (int64_t bs = 0; bs < S; bs += B) {
     const int nb = (int)std::min<int64_t>(B, S - bs);
@@ -1382,7 +1432,7 @@ int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     std::vector<Launch> sched;
     while (!fw.done())
       sched.push_back(Launch{next_pass(fw), F, F, dtc::kMeasNone, 0, 2, nullptr, 0});
-    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
+    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipStreamSynchronize(ctx->stream));  // the staged pass list is reused
   }
@@ -1393,6 +1443,7 @@ int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   ctx->prefix_n_traj = n_traj;
   ctx->prefix_len = pl.len;
   ctx->prefix_device = dv ? 1 : 0;
+  ctx->prefix_octet = octet;
   ctx->prefix_hash = prefix_hash(pr, n_periods);
   return DTC_OK;
 }
@@ -1552,9 +1603,12 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     B = std::max<int64_t>(1, std::min<int64_t>((int64_t)(budget / (dv ? 2 * per_state : per_state)),
                                                4096));
   }
-  B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
-  DTC_TRY(ensure(ctx->F, (size_t)(B * pl.len * 16)));
-  if (dv) DTC_TRY(ensure(ctx->E, (size_t)(B * pl.len * 16)));
+  int octet = 0;
+  batch_layout(ctx, S, B, octet);
+  rc.octet_bits = octet;
+  const int64_t Bp = dtc::octet_padded(B, octet);
+  DTC_TRY(ensure(ctx->F, (size_t)(Bp * pl.len * 16)));
+  if (dv) DTC_TRY(ensure(ctx->E, (size_t)(Bp * pl.len * 16)));
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_v * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
@@ -1646,7 +1700,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     double* vals = (double*)ctx->vals_f.p;
     DTC_HIP(hipMemcpyAsync(ctx->basis.p, masks.data(), nb * sizeof(int64_t),
                            hipMemcpyHostToDevice, ctx->stream));
-    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb));
+    DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_HIP(hipMemsetAsync(vals, 0, (size_t)nb * T * n_v * sizeof(double), ctx->stream));
     const int64_t vs = (int64_t)T * n_v;
     // kick records of the schedule's passes: one prep launch per segment

@@ -193,8 +193,33 @@ struct PassArgs {
   double* partial;         // [B][n_tiles][n_obs]
   const int64_t* basis;    // kick-only passes: non-null = the source is the basis state
                            // |basis[b]> (synthesised in registers: src is not read)
+  int octet_bits;          // state layout in HBM (state_addr below); 0 = contiguous
+  int lc_split, lc_tpb;    // light-cone pass variant (dev A/B, read once in dtc_open)
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
+
+// Where amplitude x of state b of a batch lives (in amplitudes from the batch
+// base).  octet_bits g = 0: b * state_len + x (contiguous states).  g > 0:
+// the states of an octet (b >> 3) are interleaved in runs of 2^g amplitudes,
+//   (b >> 3) * 8 * state_len + (b & 7) * 2^g + spread(x),
+//   spread(x) = ((x >> g) << (g + 3)) | (x & (2^g - 1)),
+// and the launch deals the eight states of an octet to consecutive blocks
+// (grid.x = 8 * tiles, grid.y = octets), i.e. one per XCD: the eight XCDs'
+// concurrent tiles then cover whole 8 * 2^g runs of memory instead of each
+// XCD streaming its own 64 KiB tiles (tools/tile_shape_bench.hip,
+// tools/pass_pattern_bench.hip: the 12-site pass's access pattern 6.2 -> 6.5
+// TB/s, the 8-site pass's 5.45 -> 5.85 at g = 6).  spread is linear over
+// disjoint bit sets, so per-register and per-lane offsets spread separately.
+__host__ __device__ __forceinline__ int64_t octet_spread(int64_t x, int g) {
+  return g ? (((x >> g) << (g + 3)) | (x & (((int64_t)1 << g) - 1))) : x;
+}
+__host__ __device__ __forceinline__ int64_t state_base(int64_t b, int64_t state_len, int g) {
+  return g ? (((b >> 3) << 3) * state_len + ((b & 7) << g)) : b * state_len;
+}
+// states a batch buffer of n states must hold (octets are padded to 8)
+__host__ __device__ __forceinline__ int64_t octet_padded(int64_t n, int g) {
+  return g ? ((n + 7) & ~(int64_t)7) : n;
+}
 
 // Kick records of n_pass passes x batch states.
 hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
@@ -208,9 +233,10 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
                          double* out, int64_t out_stride, hipStream_t stream,
                          int o_first = 0, int n_out = -1, int accumulate = 0);
 
-// state[b * state_len + idx[b]] = 1 (after the caller zeroed the batch)
+// amplitude idx[b] of state b = 1 (after the caller zeroed the batch), in the
+// batch layout of octet_bits (state_base / octet_spread)
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx,
-                            int batch, hipStream_t stream);
+                            int batch, hipStream_t stream, int octet_bits = 0);
 
 // Virtual ranks' in-place all-to-all of one slice: 2^k shards of 2^nl
 // amplitudes, chunk = top k local bits, slice = the next nl - k - nsub bits;

@@ -703,8 +703,13 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const int c = A.c, s = A.s;
   const int tile_bits = A.L_eff - kTileBits;
   const int64_t n_tiles = (int64_t)1 << tile_bits;
-  const int64_t b = blockIdx.y;
-  const int64_t tile = blockIdx.x;
+  // block -> (state, tile): octet layout: the eight states of an octet on
+  // consecutive blocks (dtc_kernels.h state_base); the padding states of a
+  // last partial octet leave at once (the whole workgroup)
+  const int og = A.octet_bits;
+  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
+  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   // this state's kick records (prep kernel), lane-distributed (RecRegs)
   RecRegs R;
@@ -749,10 +754,17 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // fits: always for layout 2 (thread bits = tile bits 0..7, L_eff <= 32),
   // for layout 1 (thread bits include tile bits 8..11) while tile bit 11's
   // global bit is <= 27 (the low group at any L; higher groups to L_eff 28) ----
-  const int64_t vofs64 = M.rel(ybase<RP::IO>(t)) << 4;
+  const int64_t vofs64 = octet_spread(M.rel(ybase<RP::IO>(t)), og) << 4;
   const uint32_t vofs = (uint32_t)vofs64;
-  const bool ofs32 = RP::IO == 2 || (c > 11 ? 11 : s + 11 - c) <= 27;
-  auto tile_ofs = [&](int r) -> int64_t { return (M.tbase | M.rel(r << (4 * RP::IO))) << 4; };
+  // the lane offset fits 32 bits while the highest lane bit's address bit is
+  // <= 27 (amplitudes): tile bit 7 (layout 2) or 11 (layout 1)
+  constexpr int kTopLaneBit = RP::IO == 2 ? 7 : 11;
+  const int top_g = kTopLaneBit < c ? kTopLaneBit : s + kTopLaneBit - c;
+  const bool ofs32 = top_g + ((og && top_g >= og) ? 3 : 0) <= 27;
+  auto tile_ofs = [&](int r) -> int64_t {
+    return octet_spread(M.tbase | M.rel(r << (4 * RP::IO)), og) << 4;
+  };
+  const int64_t sbase = state_base(b, A.state_len, og);
   double2 v[kRegs];
   bool synth = false;
   if constexpr (SHAPE == kShapeK) synth = A.basis != nullptr;
@@ -765,7 +777,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int r = 0; r < kRegs; ++r)
       v[r] = make_double2((x0 | M.rel(r << (4 * RP::IO))) == m ? 1.0 : 0.0, 0.0);
   } else {
-    const char* src = (const char*)(A.src + b * A.state_len);
+    const char* src = (const char*)(A.src + sbase);
     if (ofs32) {
 #pragma unroll
       for (int r = 0; r < kRegs; ++r) {
@@ -1120,7 +1132,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   DTC_TS(5);
 
-  char* dst = (char*)(A.dst + b * A.state_len);
+  char* dst = (char*)(A.dst + sbase);
   if constexpr (NS) {
     // measurement-only pass (the last of an echo chain): nothing to write
   } else if (ofs32) {
@@ -1269,8 +1281,10 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;  // c = 4, s = w0
   const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
-  const int64_t b = blockIdx.y;
-  const int64_t tile0 = (int64_t)blockIdx.x * TPB;
+  const int og = A.octet_bits;  // state layout, as pass_body
+  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
+  const int64_t tile0 = (og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x) * TPB;
+  if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   RecRegs R;
   {
@@ -1301,12 +1315,14 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
     if (i < kLcTab) cv[j] = ct[i];
   }
   // the tile in layout 2 (threads = tile bits 0..7: 16-amplitude runs)
-  const uint32_t vofs = (uint32_t)(M.rel(ybase<2>(t)) << 4);
-  const char* src = (const char*)(A.src + b * A.state_len);
+  // (layout 2: lanes = tile bits 0..3 (columns) and window sites 0..3; a
+  // 64-bit lane offset: the window may sit high in a large state)
+  const int64_t vofs = octet_spread(M.rel(ybase<2>(t)), og) << 4;
+  const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
   auto load_tile = [&](double2 (&dst)[kRegs], int64_t tb) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      const char* a = src + ((tb | M.rel(r << 8)) << 4) + vofs;
+      const char* a = src + (octet_spread(tb | M.rel(r << 8), og) << 4) + vofs;
       const d2v w = __builtin_nontemporal_load((const d2v*)a);
       dst[r] = make_double2(w.x, w.y);
     }
@@ -1533,20 +1549,22 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
       a.n_chunks > kMaxChunks)
     return hipErrorInvalidValue;
   const int n_tiles = 1 << (a.L_eff - kTileBits);
-  dim3 grid(n_tiles, batch);
+  if (a.octet_bits && (a.octet_bits < 4 || a.octet_bits > a.L_eff || (int64_t)n_tiles * 8 > 0x7FFFFFFF))
+    return hipErrorInvalidValue;
+  // octet layout: the eight states of an octet on consecutive blocks
+  dim3 grid = a.octet_bits ? dim3(n_tiles * 8, (batch + 7) / 8) : dim3(n_tiles, batch);
   if (shape == kShapeLC) {
     // measure-only light-cone pass: probe, window at tile bits 4..11 (c = 4)
     if (a.c != 4 || a.act != 0xFF0 || a.meas != kMeasProbe || !a.no_store || a.lc_layers < 1 ||
         a.lc_layers > kLcLayers || a.n_obs < 2 || !a.lc_diag)
       return hipErrorInvalidValue;
     // several tiles per workgroup (register double buffer) when they divide the state
-    int tpb = kLcTilesPerGroup;
-    if (const char* e = std::getenv("DTC_LC_TPB")) tpb = std::atoi(e);  // development A/B
     // default: one tile per workgroup, re-layouts through half the LDS, three
-    // workgroups per CU (r2ar: 6.15 -> 5.42 ms); DTC_LC_SPLIT=0 keeps the
-    // 64 KiB exchange and DTC_LC_TPB tiles per workgroup (development A/B)
-    const char* split_env = std::getenv("DTC_LC_SPLIT");
-    if (!(split_env && split_env[0] == '0')) {
+    // workgroups per CU (r2ar: 6.15 -> 5.42 ms); lc_split = 0 keeps the
+    // 64 KiB exchange with lc_tpb tiles per workgroup (development A/B:
+    // DTC_LC_SPLIT / DTC_LC_TPB, read once by dtc_open)
+    int tpb = a.lc_tpb > 0 ? a.lc_tpb : kLcTilesPerGroup;
+    if (a.lc_split) {
       if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
       hipLaunchKernelGGL((kind == kKindRX ? dtc_lc_final_split<kKindRX> : dtc_lc_final_split<kKindRY>),
                          grid, dim3(kThreads), 0, stream, a);
@@ -1554,7 +1572,7 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
     }
     while (tpb > 1 && n_tiles % tpb) tpb >>= 1;
     if (tpb != 1 && tpb != 2 && tpb != 4) tpb = 1;
-    grid.x = n_tiles / tpb;
+    grid.x = (a.octet_bits ? 8 : 1) * n_tiles / tpb;
     if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
     const bool rx = kind == kKindRX;
     if (tpb == 4)
@@ -1627,16 +1645,16 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
 }
 
 __global__ void set_basis_kernel(double2* state, int64_t state_len, const int64_t* idx,
-                                 int batch) {
+                                 int batch, int og) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
-  state[(int64_t)b * state_len + idx[b]] = make_double2(1.0, 0.0);
+  state[state_base(b, state_len, og) + octet_spread(idx[b], og)] = make_double2(1.0, 0.0);
 }
 
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx, int batch,
-                            hipStream_t stream) {
+                            hipStream_t stream, int octet_bits) {
   hipLaunchKernelGGL(set_basis_kernel, dim3((batch + 63) / 64), dim3(64), 0, stream, state,
-                     state_len, idx, batch);
+                     state_len, idx, batch, octet_bits);
   return hipGetLastError();
 }
 

@@ -1,0 +1,147 @@
+// Pass-pattern study, round 3 (not part of the product).  tile_shape_bench
+// found a 64 KiB-per-workgroup in-place sweep at 6.5 TB/s when the eight
+// workgroups that the dispatcher deals to the eight XCDs (consecutive block
+// ids) read disjoint residues of the 4 KiB piece index mod 8 -- each XCD then
+// streams from one residue class -- and at 5.2-5.4 TB/s when each workgroup's
+// 64 KiB is contiguous.  This replays the pass kernels' exact access pattern
+// (L=20 states, a 4096-amplitude tile = tile bits [0, c) + [s, s + 12 - c),
+// the IO register layouts, 16 nontemporal 16-B loads and stores per lane, in
+// place) for:
+//   group A  c = 12 (sites 0..11), IO layout 1 (lanes = tile bits 0..3, 8..11)
+//   group B  c = 4, s = 12 (column bits 0..3 + sites 12..19), IO layout 2
+// under
+//   state layout 0: state b at b * 2^L (contiguous)
+//   state layout 1: octets of states interleaved at 4 KiB: amplitude x of
+//                   state b at ((b >> 3) 2^L + (x >> 8) 2^11 + (b & 7) 2^8 + (x & 255))
+// and block orders (linear block id -> (state, tile id)):
+//   order 0: tile id fastest (the kernels' grid(n_tiles, batch))
+//   order 1: state bits 0..2 fastest, then tile id, then the rest of the state
+//   order 2: group B only: the tile-id bits that are index bits 8..10 fastest
+// Build: hipcc --offload-arch=gfx950 -O3 tools/pass_pattern_bench.hip -o tools/pass_pattern_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define CHECK(x)                                                         \
+  do {                                                                   \
+    hipError_t e = (x);                                                  \
+    if (e != hipSuccess) {                                               \
+      printf("%s: %s\n", #x, hipGetErrorString(e));                      \
+      return 1;                                                          \
+    }                                                                    \
+  } while (0)
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+struct Pat {
+  int L, c, s, io, layout, order, batch, gbits, ro;
+};
+
+// layout 1: octets of states interleaved at 2^gbits amplitudes
+__device__ __forceinline__ int64_t addr_of(const Pat& P, int64_t st, int64_t x) {
+  if (P.layout == 0) return (st << P.L) + x;
+  const int g = P.gbits;
+  return ((st >> 3) << (P.L + 3)) + ((x >> g) << (g + 3)) + ((st & 7) << g) +
+         (x & ((1 << g) - 1));
+}
+
+__global__ __launch_bounds__(256, 2) void k_pass(d2v* __restrict__ a, Pat P, double f) {
+  __shared__ d2v s_pad[4096];  // the pass kernels' 64 KiB LDS tile: 2 workgroups per CU
+  const int t = threadIdx.x;
+  const int tile_bits = P.L - 12;
+  const int64_t n_tiles = (int64_t)1 << tile_bits;
+  int64_t b = blockIdx.x;
+  int64_t tile, st;
+  if (P.order == 0) {
+    tile = b & (n_tiles - 1);
+    st = b >> tile_bits;
+  } else if (P.order == 1) {
+    const int64_t lo = b & 7;
+    tile = (b >> 3) & (n_tiles - 1);
+    st = ((b >> (3 + tile_bits)) << 3) | lo;
+  } else {
+    // tile-id bits (4..6) = index bits 8..10 of a c = 4 tile fastest
+    const int64_t lo = b & 7, rest = b >> 3;
+    tile = (rest & 15) | (lo << 4) | (((rest >> 4) & ((n_tiles >> 7) - 1)) << 7);
+    st = rest >> (tile_bits - 3);
+  }
+  const int mid_bits = P.s - P.c;
+  const int64_t mid_mask = ((int64_t)1 << mid_bits) - 1;
+  const int64_t tbase = ((tile & mid_mask) << P.c) | ((tile >> mid_bits) << (P.s + 12 - P.c));
+  auto rel = [&](int y) -> int64_t {
+    return (int64_t)(y & ((1 << P.c) - 1)) | ((int64_t)(y >> P.c) << P.s);
+  };
+  auto ty = [&](int r) -> int {
+    // tile-local index of register r of thread t in the IO layout
+    if (P.io == 1) return (t & 15) | (r << 4) | ((t >> 4) << 8);
+    return t | (r << 8);
+  };
+  d2v v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = __builtin_nontemporal_load(&a[addr_of(P, st, tbase | rel(ty(r)))]);
+  if (f == 12345.0) s_pad[t] = v[0];
+  if (P.ro) {  // read only (the light-cone pass)
+    d2v acc = v[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) acc += v[r];
+    if (acc.x == 12345.0) a[0] = acc;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    __builtin_nontemporal_store(v[r] * (1.0 + f), &a[addr_of(P, st, tbase | rel(ty(r)))]);
+}
+
+template <typename F>
+float time_it(F fn, int reps) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  fn();
+  fn();
+  (void)hipEventRecord(e0);
+  for (int i = 0; i < reps; ++i) fn();
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms / reps;
+}
+
+int main() {
+  const int L = 20, B = 512;  // 8 GiB
+  const size_t n = (size_t)B << L;
+  d2v* a;
+  CHECK(hipMalloc(&a, n * 16));
+  CHECK(hipMemset(a, 0, n * 16));
+  struct Case {
+    const char* name;
+    Pat p;
+  } cases[] = {
+      {"A c=12 io1 contiguous  order0", {L, 12, 12, 1, 0, 0, B, 8, 0}},
+      {"A c=12 io1 il4K        order1", {L, 12, 12, 1, 1, 1, B, 8, 0}},
+      {"A c=12 io1 il1K        order1", {L, 12, 12, 1, 1, 1, B, 6, 0}},
+      {"A c=12 io1 il256       order1", {L, 12, 12, 1, 1, 1, B, 4, 0}},
+      {"A c=12 io1 il64K       order1", {L, 12, 12, 1, 1, 1, B, 12, 0}},
+      {"B c=4  io2 contiguous  order0", {L, 4, 12, 2, 0, 0, B, 8, 0}},
+      {"B c=4  io2 contiguous  order2", {L, 4, 12, 2, 0, 2, B, 8, 0}},
+      {"B c=4  io2 il4K        order1", {L, 4, 12, 2, 1, 1, B, 8, 0}},
+      {"B c=4  io2 il1K        order1", {L, 4, 12, 2, 1, 1, B, 6, 0}},
+      {"B c=4  io2 il256       order1", {L, 4, 12, 2, 1, 1, B, 4, 0}},
+      {"B c=4  io2 il64K       order1", {L, 4, 12, 2, 1, 1, B, 12, 0}},
+      {"B c=4  io1 il256       order1", {L, 4, 12, 1, 1, 1, B, 4, 0}},
+      {"B c=4  io1 contiguous  order0", {L, 4, 12, 1, 0, 0, B, 8, 0}},
+      {"LC w0=6 read contiguous order0", {L, 4, 6, 2, 0, 0, B, 8, 1}},
+      {"LC w0=6 read il4K      order1", {L, 4, 6, 2, 1, 1, B, 8, 1}},
+      {"LC w0=6 read il256     order1", {L, 4, 6, 2, 1, 1, B, 4, 1}},
+      {"read A  contiguous      order0", {L, 12, 12, 2, 0, 0, B, 8, 1}},
+      {"read A  il4K            order1", {L, 12, 12, 2, 1, 1, B, 8, 1}},
+  };
+  const unsigned blocks = (unsigned)(n / 4096);
+  for (auto& cs : cases) {
+    const float ms = time_it([&] { hipLaunchKernelGGL(k_pass, dim3(blocks), dim3(256), 0, 0, a, cs.p, 0.0); }, 8);
+    printf("%-34s %8.3f ms %7.0f GB/s\n", cs.name, ms, (cs.p.ro ? 1.0 : 2.0) * n * 16 / ms / 1e6);
+    fflush(stdout);
+  }
+  return 0;
+}

@@ -14,6 +14,6 @@ for set in \
   "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VMEM" \
   "GRBM_GUI_ACTIVE GRBM_COUNT" ; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d $O -o p$i -- python $R/bench.py --steps 1 --warmup 0 --strong-total 0 --batch 64 --no-cpu-baseline > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d $O -o p$i -- python $R/bench.py --steps 1 --warmup 0 --strong-total 0 --batch ${B:-64} --no-cpu-baseline $BENCH_ARGS > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
 echo done

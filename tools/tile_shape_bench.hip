@@ -39,7 +39,13 @@ __device__ __forceinline__ size_t piece(size_t b, size_t nb, int u) {
   }
   if constexpr (MAP == 2) return (size_t)u * nb + b;
   // MAP 3: the 8 consecutive blocks (one per XCD) take 8 consecutive pieces
-  return ((b / 8) * 16 + u) * 8 + (b % 8);
+  if constexpr (MAP == 3) return ((b / 8) * 16 + u) * 8 + (b % 8);
+  // MAP 4: as 3, residues permuted among the eight
+  if constexpr (MAP == 4) return ((b / 8) * 16 + u) * 8 + ((b % 8) * 3 % 8);
+  // MAP 5: adjacent like 3, but each workgroup's residue rotates per load
+  if constexpr (MAP == 5) return ((b / 8) * 16 + u) * 8 + ((b + u) % 8);
+  // MAP 6: residue b % 8 like 3, the eight far apart (1/16 of the array)
+  return ((size_t)u * (nb / 8) + b / 8) * 8 + (b % 8);
 }
 
 template <int MAP, int LDSKB, int EXCH, int WPC>
@@ -117,6 +123,9 @@ int main() {
   run<1, 64, 0, 2>("2 WG/CU");
   run<2, 64, 0, 2>("2 WG/CU");
   run<3, 64, 0, 2>("2 WG/CU");
+  run<4, 64, 0, 2>("2 WG/CU");
+  run<5, 64, 0, 2>("2 WG/CU");
+  run<6, 64, 0, 2>("2 WG/CU");
   run<0, 64, 4, 2>("2 WG/CU");
   run<1, 64, 4, 2>("2 WG/CU");
   run<2, 64, 4, 2>("2 WG/CU");
