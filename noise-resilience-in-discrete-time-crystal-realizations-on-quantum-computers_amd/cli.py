@@ -65,6 +65,10 @@ def build_parser():
                    help="periods at time t = t + t_offset (1 for the controlled-g scripts)")
     p.add_argument("--gate_counts", type=int, default=0, help="also write gate_counts_*.csv")
     p.add_argument("--batch", type=int, default=0, help="states per device batch (0 = auto)")
+    p.add_argument("--independent_t", type=int, default=0,
+                   help="1 = every t from its own trajectories (uncorrelated across t, as the "
+                        "reference's circuit per t, fast.py:219-221; O(T^2) periods); 0 = the "
+                        "echo branches off one forward trajectory (correlated across t)")
     return p
 
 
@@ -98,11 +102,13 @@ def main(argv=None):
     if world > 1:
         from .distributed import sharded_sweep
 
-        res = sharded_sweep(spec, n_traj, shots=shots, seed=args.seed, batch=args.batch)
+        res = sharded_sweep(spec, n_traj, shots=shots, seed=args.seed, batch=args.batch,
+                            independent_t=bool(args.independent_t))
         if rank != 0:
             return 0
     else:
-        res = sw.run_sweep(spec, n_traj=n_traj, shots=shots, seed=args.seed, batch=args.batch)
+        res = sw.run_sweep(spec, n_traj=n_traj, shots=shots, seed=args.seed, batch=args.batch,
+                           independent_t=bool(args.independent_t))
     elapsed = time.time() - t0
     print(f"Completed forward+echo sweep in {elapsed:.2f}s "
           f"({spec.n_inst} instance(s) x {n_traj} trajectories x {T} times)")

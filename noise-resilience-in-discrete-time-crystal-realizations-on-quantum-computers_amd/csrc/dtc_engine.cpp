@@ -96,6 +96,7 @@ struct dtc_ctx {
   int octet_bits = 6;        // DTC_OCTET_BITS (0 = contiguous states)
   int lc_split = 1;          // DTC_LC_SPLIT
   int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
+  int kdk_split = 1 << 7;    // DTC_KDK_SPLIT: nibble-set mask of the 3-per-CU K-D-K
   bool basis_synth = true;   // DTC_NO_BASIS_SYNTH
   bool lightcone = true;     // DTC_NO_LIGHTCONE
   double batch_bytes = 0.0;  // DTC_BATCH_BYTES (0 = automatic)
@@ -376,6 +377,7 @@ dtc::PassArgs base_args(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start) {
   A.octet_bits = rc.octet_bits;
   A.lc_split = ctx->lc_split;
   A.lc_tpb = ctx->lc_tpb;
+  A.kdk_split = ctx->kdk_split;
 #ifdef DTC_PHASE_TIMING
   if (const char* e = std::getenv("DTC_DBG_PTR")) A.dbg_ts = (uint64_t*)std::strtoull(e, nullptr, 0);
 #endif
@@ -984,6 +986,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   if (c->octet_bits != 0 && (c->octet_bits < 4 || c->octet_bits > 12)) c->octet_bits = 6;
   if (const char* e = std::getenv("DTC_LC_SPLIT")) c->lc_split = e[0] != '0';
   if (const char* e = std::getenv("DTC_LC_TPB")) c->lc_tpb = std::atoi(e);
+  if (const char* e = std::getenv("DTC_KDK_SPLIT")) c->kdk_split = std::atoi(e);
   c->basis_synth = std::getenv("DTC_NO_BASIS_SYNTH") == nullptr;
   c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
   if (const char* e = std::getenv("DTC_BATCH_BYTES")) c->batch_bytes = std::atof(e);

@@ -509,6 +509,13 @@ __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_ha
   for (int r = 0; r < kRegs; ++r) v[r].y = s_half[lds_slot8(tile_y<TO>(t, r))];
 }
 
+template <bool SPLIT, int FROM, int TO>
+__device__ __forceinline__ void xch_tile(double2 (&v)[kRegs], double2* s_tile, double* s_half,
+                                         int t) {
+  if constexpr (SPLIT) exchange_split<FROM, TO>(v, s_half, t);
+  else exchange<FROM, TO>(v, s_tile, t);
+}
+
 __device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chunks, int64_t x) {
   double2 ph = s_chunk[x & 63];
   for (int k = 1; k < n_chunks; ++k) {
@@ -685,7 +692,9 @@ struct RoundPlan {
 // MC, the measurements compiled in (separate instantiations, so a pass
 // carries only the code it can run): 0 = none, 1 = the probe, 2 = any mode
 // (per-site / energy Z), 3 = energy with the in-flight <X> points.
-template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false>
+// SPLIT: re-layouts through a 32 KiB half-tile buffer (exchange_split), so a
+// third workgroup fits a CU (dtc_kdk_pass3; development A/B, PassArgs::kdk_split)
+template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false, bool SPLIT = false>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
@@ -694,7 +703,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
   DTC_TS(0);
-  __shared__ double2 s_tile[kTile];
+  __shared__ double2 s_tile[SPLIT ? 1 : kTile];
+  __shared__ double s_half[SPLIT ? kTile : 1];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
   __shared__ double s_red[kThreads / 64][kRedSlots];
@@ -1074,13 +1084,13 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       if (x_pre) sc *= nib_w2(RP::IO, 0);
     }
     if constexpr (RP::n0) {
-      exchange<RP::IO, 0>(v, s_tile, t);
+      xch_tile<SPLIT, RP::IO, 0>(v, s_tile, s_half, t);
       if (x_pre) measure_x_pre(L0{}, sc);
       apply_nibble<0, KIND>(v, R, 0);
       if (x_pre) sc *= nib_w2(0, 0);
     }
     if constexpr (RP::nO) {
-      exchange<RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, t);
+      xch_tile<SPLIT, RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, s_half, t);
       if (x_pre) measure_x_pre(LO{}, sc);
       apply_nibble<RP::O, KIND>(v, R, 0);
     }
@@ -1107,25 +1117,25 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (RP::post) {
     double sc = inv_w2_mid;
     if constexpr (RP::nO) {
-      exchange<RP::d_lay, RP::O>(v, s_tile, t);
+      xch_tile<SPLIT, RP::d_lay, RP::O>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(LO{}, sc);
       apply_nibble<RP::O, KIND>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(RP::O, kTileBits);
     }
     if constexpr (RP::n0) {
-      exchange<RP::pO, 0>(v, s_tile, t);
+      xch_tile<SPLIT, RP::pO, 0>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(L0{}, sc);
       apply_nibble<0, KIND>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(0, kTileBits);
     }
     if constexpr (RP::nIO) {
-      exchange<RP::p0, RP::IO>(v, s_tile, t);
+      xch_tile<SPLIT, RP::p0, RP::IO>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(LIO{}, sc);
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
-    exchange<RP::pIO, RP::IO>(v, s_tile, t);
+    xch_tile<SPLIT, RP::pIO, RP::IO>(v, s_tile, s_half, t);
   } else {
-    exchange<RP::d_lay, RP::IO>(v, s_tile, t);
+    xch_tile<SPLIT, RP::d_lay, RP::IO>(v, s_tile, s_half, t);
   }
   if constexpr (MC > 0) {
     if (A.meas != kMeasNone && A.meas_at_end) measure_in(LIO{}, 1.0);
@@ -1227,6 +1237,13 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     pass_body<SHAPE_EXPR, NIBS, KIND, MC>(A);                                      \
   }
 DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
+// the K-D-K at three workgroups per CU (half-LDS re-layouts, 168 VGPRs) for
+// the nibble sets in PassArgs::kdk_split (bit NIBS; default: the 12-site group,
+// r3g same-box A/B with the octet layout: <7> 6.10 -> 5.87 ms, <6> 5.79 -> 5.90)
+template <int NIBS, int KIND, int MC>
+__global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
+  pass_body<kShapeKDK, NIBS, KIND, MC, false, true>(A);
+}
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
 DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
@@ -1496,7 +1513,15 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     }
   }
   switch (shape) {
-    case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeKDK:
+      if constexpr (MC <= 1) {
+        if ((a.kdk_split >> NIBS) & 1) {
+          hipLaunchKernelGGL((dtc_kdk_pass3<NIBS, KIND, MC>), grid, block, 0, stream, a);
+          break;
+        }
+      }
+      hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a);
+      break;
     case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
     case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
     case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;

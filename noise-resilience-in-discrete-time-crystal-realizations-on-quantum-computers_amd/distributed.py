@@ -64,10 +64,12 @@ def sub_spec(spec: SweepSpec, lo: int, hi: int) -> SweepSpec:
 
 
 def sharded_sweep(spec: SweepSpec, n_traj: int, shots=None, seed=0x5EED0001, batch=0,
-                  want_fwd=True, want_echo=True, want_zsite=False, shard="auto", engine=None):
+                  want_fwd=True, want_echo=True, want_zsite=False, shard="auto", engine=None,
+                  independent_t=False):
     """Sweep sharded over the torch.distributed world: by trajectory blocks, or
     (``shard="instances"``, default when n_traj < world) by instance blocks.
-    Either way the per-trajectory values are those of a single-process run."""
+    Either way the per-trajectory values are those of a single-process run
+    (``independent_t``: sweep.autocorr_independent_t per block)."""
     import torch.distributed as dist
 
     from . import sweep as sw
@@ -92,6 +94,10 @@ def sharded_sweep(spec: SweepSpec, n_traj: int, shots=None, seed=0x5EED0001, bat
         def compute(lo, hi):
             if hi <= lo:
                 return empty(0, n_traj)
+            if independent_t:
+                return sw.autocorr_independent_t(eng, sub_spec(spec, lo, hi), n_traj, seed=seed,
+                                                 want_fwd=want_fwd, want_echo=want_echo,
+                                                 batch=batch)
             return eng.autocorr(sub_spec(spec, lo, hi), n_traj, seed=seed, want_fwd=want_fwd,
                                 want_echo=want_echo, want_zsite=want_zsite, batch=batch)
 
@@ -100,6 +106,10 @@ def sharded_sweep(spec: SweepSpec, n_traj: int, shots=None, seed=0x5EED0001, bat
         def compute(lo, hi):
             if hi <= lo:
                 return empty(spec.n_inst, 0)
+            if independent_t:
+                return sw.autocorr_independent_t(eng, spec, hi - lo, seed=seed, lo=lo,
+                                                 n_total=n_traj, want_fwd=want_fwd,
+                                                 want_echo=want_echo, batch=batch)
             return eng.autocorr(spec, hi - lo, seed=seed, traj_offset=lo, want_fwd=want_fwd,
                                 want_echo=want_echo, want_zsite=want_zsite, batch=batch)
 

@@ -74,16 +74,52 @@ def _shot_estimate(a: np.ndarray, shots: int, rng: np.random.Generator) -> np.nd
     return (2.0 * zero.sum(axis=1) - shots) / shots
 
 
+def autocorr_independent_t(eng, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
+                           lo: int = 0, n_total: int | None = None, want_fwd=True,
+                           want_echo=True, batch: int = 0) -> dict:
+    """Per-trajectory outputs like ``eng.autocorr``, but every time point from
+    its own trajectories, as the reference's fresh circuit per t
+    (autocorr-delta-a-single-qiskit-fast.py:219-221): point t runs a sweep of
+    t + t_offset periods that measures only t (``t_first``), with trajectory ids
+    t * n_total + lo .. (+ n_traj) -- distinct Philox streams for every t, so
+    the points are uncorrelated across t and a run sharded over trajectory
+    blocks [lo, lo + n_traj) of n_total gives the same values.  Costs O(T^2)
+    period applications instead of O(T^2 / 2) shared with the forward branch:
+    about 2 t periods per trajectory for point t."""
+    n_total = n_traj if n_total is None else n_total
+    n_inst, T = spec.n_inst, spec.T
+    out = {}
+    if want_fwd:
+        out["fwd"] = np.zeros((n_inst, n_traj, T))
+    if want_echo:
+        out["echo"] = np.zeros((n_inst, n_traj, T))
+    for t in range(T):
+        rows = max(1, t + spec.t_offset)
+        s_t = dataclasses.replace(spec, T=t + 1, kick=spec.kick[:rows])
+        r = eng.autocorr(s_t, n_traj, seed=seed, traj_offset=t * n_total + lo,
+                         want_fwd=want_fwd, want_echo=want_echo, batch=batch, t_first=t)
+        for k in out:
+            out[k][:, :, t] = r[k][:, :, t]
+    return out
+
+
 def run_sweep(spec: SweepSpec, n_traj: int | None = None, shots: int | None = None,
               engine: DtcEngine | None = None, seed: int = 0x5EED0001, want_fwd=True,
               want_echo=True, want_zsite=False, traj_offset: int = 0,
-              batch: int = 0) -> SweepResult:
-    """All t of all instances in one engine call."""
+              batch: int = 0, independent_t: bool = False) -> SweepResult:
+    """All t of all instances in one engine call (``independent_t``: one call
+    per t with its own trajectories, ``autocorr_independent_t``)."""
     eng = engine or _default_engine()
     if n_traj is None:
         n_traj = 1 if (spec.p == 0 and spec.device is None) else (shots or 1024)
-    out = eng.autocorr(spec, n_traj, seed=seed, traj_offset=traj_offset, want_fwd=want_fwd,
-                       want_echo=want_echo, want_zsite=want_zsite, batch=batch)
+    if independent_t:
+        if want_zsite:
+            raise ValueError("independent_t: per-site Z is a forward-sweep output")
+        out = autocorr_independent_t(eng, spec, n_traj, seed=seed, lo=traj_offset,
+                                     want_fwd=want_fwd, want_echo=want_echo, batch=batch)
+    else:
+        out = eng.autocorr(spec, n_traj, seed=seed, traj_offset=traj_offset, want_fwd=want_fwd,
+                           want_echo=want_echo, want_zsite=want_zsite, batch=batch)
     rng = np.random.default_rng(seed)
     res = {}
     for key in ("fwd", "echo"):

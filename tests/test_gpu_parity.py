@@ -222,3 +222,27 @@ def test_echo_light_cone_end(pkg, engine, monkeypatch, L, T, p, state, pol, toff
     full = engine.autocorr(spec, 3, seed=77)
     assert np.abs(got["echo"] - full["echo"]).max() < 1e-12
     assert np.abs(got["fwd"] - full["fwd"]).max() == 0.0
+
+
+def test_independent_t_matches_oracle(pkg, engine):
+    """--independent_t: every t from its own trajectories (t_first runs of
+    t + t_offset periods, fast.py:219-221) -- engine = C oracle per trajectory."""
+    from oracle import c_oracle
+
+    rng = np.random.default_rng(31)
+    L, T, n = 13, 6, 4
+    hs = rng.uniform(-np.pi, np.pi, (1, L))
+    phis = rng.uniform(-1.5 * np.pi, -0.5 * np.pi, (1, L - 1))
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=0.07,
+                         initial_state="neel", polarization="xy")
+
+    class Oracle:
+        def autocorr(self, spec, n_traj, seed=0x5EED0001, traj_offset=0, want_fwd=True,
+                     want_echo=True, want_zsite=False, batch=0, t_first=0):
+            return c_oracle.autocorr(spec, n_traj, seed=seed, traj_offset=traj_offset,
+                                     want_fwd=want_fwd, want_echo=want_echo, t_first=t_first)
+
+    got = pkg.sweep.autocorr_independent_t(engine, spec, n, seed=5)
+    ref = pkg.sweep.autocorr_independent_t(Oracle(), spec, n, seed=5)
+    for k in ("fwd", "echo"):
+        assert np.abs(got[k] - ref[k]).max() < 1e-10
