@@ -493,20 +493,36 @@ __device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, i
 // conflict-free): half the LDS, so three workgroups fit a CU; two more
 // barriers (the imaginary writes reuse the slots the real reads just left).
 __device__ __forceinline__ int lds_slot8(int y) { return y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4); }
+// lds_slot8(tile_y<LAY>(t, r)) = slot8_of<LAY>(lds_slot8(ybase<LAY>(t)), r): the
+// register part is a compile-time XOR (layouts 0, 1) or an XOR of bit 4 plus an
+// offset (layout 2) on a per-thread base
+template <int LAY>
+__device__ __forceinline__ int slot8_of(int base, int r) {
+  if (LAY == 0) return base ^ r;
+  if (LAY == 1) return base ^ (17 * r);
+  return (base ^ ((r & 1) << 4)) | (r << 8);
+}
 template <int FROM, int TO>
 __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t) {
   if (FROM == TO) return;
+  // the two per-thread bases are made opaque here, so every exchange forms its
+  // slots afresh (one XOR each) instead of the compiler keeping 16 slot
+  // addresses per layout live across the kernel (48 VGPRs: the 12-site K-D-K
+  // at three workgroups per CU spilled 80 B/lane for them, r3h PMC: +24 % HBM
+  // writes)
+  int bf = lds_slot8(ybase<FROM>(t)), bt = lds_slot8(ybase<TO>(t));
+  asm volatile("" : "+v"(bf), "+v"(bt));
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_half[lds_slot8(tile_y<FROM>(t, r))] = v[r].x;
+  for (int r = 0; r < kRegs; ++r) s_half[slot8_of<FROM>(bf, r)] = v[r].x;
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r].x = s_half[lds_slot8(tile_y<TO>(t, r))];
+  for (int r = 0; r < kRegs; ++r) v[r].x = s_half[slot8_of<TO>(bt, r)];
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_half[lds_slot8(tile_y<FROM>(t, r))] = v[r].y;
+  for (int r = 0; r < kRegs; ++r) s_half[slot8_of<FROM>(bf, r)] = v[r].y;
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r].y = s_half[lds_slot8(tile_y<TO>(t, r))];
+  for (int r = 0; r < kRegs; ++r) v[r].y = s_half[slot8_of<TO>(bt, r)];
 }
 
 template <bool SPLIT, int FROM, int TO>
