@@ -96,7 +96,9 @@ struct dtc_ctx {
   int octet_bits = 6;        // DTC_OCTET_BITS (0 = contiguous states)
   int lc_split = 1;          // DTC_LC_SPLIT
   int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
-  int kdk_split = 1 << 7;    // DTC_KDK_SPLIT: nibble-set mask of the 3-per-CU K-D-K
+  // DTC_KDK_SPLIT: which K-D-K passes run three workgroups per CU (dtc_kernels.h
+  // PassArgs::kdk_split): the 12-site probe passes, every per-site/energy pass
+  int kdk_split = (1 << 7) | (1 << (8 + 7)) | (1 << (8 + 6));
   bool basis_synth = true;   // DTC_NO_BASIS_SYNTH
   bool lightcone = true;     // DTC_NO_LIGHTCONE
   double batch_bytes = 0.0;  // DTC_BATCH_BYTES (0 = automatic)

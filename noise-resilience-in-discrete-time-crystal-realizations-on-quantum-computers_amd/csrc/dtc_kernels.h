@@ -195,7 +195,8 @@ struct PassArgs {
                            // |basis[b]> (synthesised in registers: src is not read)
   int octet_bits;          // state layout in HBM (state_addr below); 0 = contiguous
   int lc_split, lc_tpb;    // light-cone pass variant (dev A/B, read once in dtc_open)
-  int kdk_split;           // bit NIBS: that K-D-K at three workgroups per CU (dtc_kdk_pass3)
+  int kdk_split;           // K-D-K at three workgroups per CU (dtc_kdk_pass3): bit NIBS for
+                           // measurement classes 0/1, bit 8 + NIBS for 2/3
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
 

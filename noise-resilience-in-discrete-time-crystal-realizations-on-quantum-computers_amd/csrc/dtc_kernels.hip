@@ -1063,15 +1063,28 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // X before a pre- or post-kick nibble: each thread's pair sums only; their
   // wave reductions run after the tile's stores are issued (the pre-kick sums
   // stay live across the diagonal: 245 VGPRs, still 2 waves per SIMD)
-  double xpost[3][4];
+  // (SPLIT, three workgroups per CU at 168 VGPRs: the 24 deferred sums do not
+  // fit, so each X point is reduced into s_red at once; the slots are distinct
+  // per point and read after the stores' barrier as in the deferred form)
+  double xpost[SPLIT ? 1 : 3][4];
+  double xpre[SPLIT ? 1 : 3][4];
+  auto x_now = [&](auto lay_tag, double scale, int slot0) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    double a[4];
+    pair_sums(lay_tag, a, scale);
+    const double k = wave_sum_multi<4>(a);
+    const int lane = t & 63;
+    if ((lane & 15) == 0) s_red[t >> 6][slot0 + 4 * LAY + (lane >> 4)] = k;
+  };
   auto measure_x_post = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
-    pair_sums(lay_tag, xpost[LAY], scale);
+    if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPost);
+    else pair_sums(lay_tag, xpost[LAY], scale);
   };
-  double xpre[3][4];
   auto measure_x_pre = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
-    pair_sums(lay_tag, xpre[LAY], scale);
+    if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPre);
+    else pair_sums(lay_tag, xpre[LAY], scale);
   };
   // squared share of the global factor carried by the factored kicks of
   // nibble N (records rec0 + 4N .. +3): measuring after them multiplies sums by
@@ -1189,7 +1202,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
   if constexpr (MC >= 2) {
     // measurement combines after the tile's stores are issued (one barrier)
-    if constexpr (MC == 3) {
+    if constexpr (MC == 3 && !SPLIT) {
       const int wave = t >> 6, lane = t & 63;
       auto finish = [&](auto lay_tag, double (&xs)[3][4], int slot0) {
         constexpr int LAY = decltype(lay_tag)::value;
@@ -1254,8 +1267,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   }
 DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
 // the K-D-K at three workgroups per CU (half-LDS re-layouts, 168 VGPRs) for
-// the nibble sets in PassArgs::kdk_split (bit NIBS; default: the 12-site group,
-// r3g same-box A/B with the octet layout: <7> 6.10 -> 5.87 ms, <6> 5.79 -> 5.90)
+// the nibble sets in PassArgs::kdk_split: bit NIBS for passes without or with
+// the probe measurement, bit 8 + NIBS for per-site / energy ones.  Default: the
+// 12-site probe passes (r3i: <7> 5.36 ms vs 6.10; the 8-site ones are 2 %
+// slower at three) and every per-site / energy pass (r3r: energy K-D-K 1.81 ->
+// 1.69 ms at B=256, C4 +1 %)
 template <int NIBS, int KIND, int MC>
 __global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
   pass_body<kShapeKDK, NIBS, KIND, MC, false, true>(A);
@@ -1530,8 +1546,8 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
   }
   switch (shape) {
     case kShapeKDK:
-      if constexpr (MC <= 1) {
-        if ((a.kdk_split >> NIBS) & 1) {
+      if constexpr (true) {
+        if ((a.kdk_split >> (NIBS + (MC >= 2 ? 8 : 0))) & 1) {
           hipLaunchKernelGGL((dtc_kdk_pass3<NIBS, KIND, MC>), grid, block, 0, stream, a);
           break;
         }

@@ -59,6 +59,17 @@ __global__ __launch_bounds__(256, 2) void k_pass(d2v* __restrict__ a, Pat P, dou
     const int64_t lo = b & 7;
     tile = (b >> 3) & (n_tiles - 1);
     st = ((b >> (3 + tile_bits)) << 3) | lo;
+  } else if (P.order == 3) {
+    // tile-id bits 0, 1 fastest, then state bit 0, then state bits 1, 2, then
+    // the rest of the tile id, then the rest of the state
+    const int64_t t01 = b & 3, s0 = (b >> 2) & 1, s12 = (b >> 3) & 3, rest = b >> 5;
+    tile = t01 | ((rest & ((n_tiles >> 2) - 1)) << 2);
+    st = (((rest >> (tile_bits - 2)) << 3) | (s12 << 1) | s0);
+  } else if (P.order == 4) {
+    // tile-id bits 0, 1 fastest, then state & 7, then the rest
+    const int64_t t01 = b & 3, s7 = (b >> 2) & 7, rest = b >> 5;
+    tile = t01 | ((rest & ((n_tiles >> 2) - 1)) << 2);
+    st = ((rest >> (tile_bits - 2)) << 3) | s7;
   } else {
     // tile-id bits (4..6) = index bits 8..10 of a c = 4 tile fastest
     const int64_t lo = b & 7, rest = b >> 3;
@@ -92,6 +103,36 @@ __global__ __launch_bounds__(256, 2) void k_pass(d2v* __restrict__ a, Pat P, dou
     __builtin_nontemporal_store(v[r] * (1.0 + f), &a[addr_of(P, st, tbase | rel(ty(r)))]);
 }
 
+// Larger tiles for the 8-site group: 2^(12+E) amplitudes = c column bits +
+// the 8 sites, 256 << E threads x 16 registers (threads = the low tile bits),
+// octet layout at 1 KiB, order 1 (state & 7 fastest)
+template <int E>
+__global__ __launch_bounds__(256 << E) void k_big(d2v* __restrict__ a, int L, int c, int s0,
+                                                  double f) {
+  constexpr int TB = 12 + E;
+  const int t = threadIdx.x;
+  const int tile_bits = L - TB;
+  const int64_t n_tiles = (int64_t)1 << tile_bits;
+  const int64_t b = blockIdx.x;
+  const int64_t tile = (b >> 3) & (n_tiles - 1);
+  const int64_t st = ((b >> (3 + tile_bits)) << 3) | (b & 7);
+  const int mid_bits = s0 - c;
+  const int64_t mid_mask = ((int64_t)1 << mid_bits) - 1;
+  const int64_t tbase = ((tile & mid_mask) << c) | ((tile >> mid_bits) << (s0 + TB - c));
+  auto rel = [&](int y) -> int64_t {
+    return (int64_t)(y & ((1 << c) - 1)) | ((int64_t)(y >> c) << s0);
+  };
+  auto addr = [&](int64_t x) -> int64_t {
+    return ((st >> 3) << (L + 3)) + ((x >> 6) << 9) + ((st & 7) << 6) + (x & 63);
+  };
+  d2v v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = __builtin_nontemporal_load(&a[addr(tbase | rel(t | (r << (8 + E))))]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    __builtin_nontemporal_store(v[r] * (1.0 + f), &a[addr(tbase | rel(t | (r << (8 + E))))]);
+}
+
 template <typename F>
 float time_it(F fn, int reps) {
   hipEvent_t e0, e1;
@@ -118,30 +159,27 @@ int main() {
     const char* name;
     Pat p;
   } cases[] = {
-      {"A c=12 io1 contiguous  order0", {L, 12, 12, 1, 0, 0, B, 8, 0}},
-      {"A c=12 io1 il4K        order1", {L, 12, 12, 1, 1, 1, B, 8, 0}},
       {"A c=12 io1 il1K        order1", {L, 12, 12, 1, 1, 1, B, 6, 0}},
-      {"A c=12 io1 il256       order1", {L, 12, 12, 1, 1, 1, B, 4, 0}},
-      {"A c=12 io1 il64K       order1", {L, 12, 12, 1, 1, 1, B, 12, 0}},
-      {"B c=4  io2 contiguous  order0", {L, 4, 12, 2, 0, 0, B, 8, 0}},
-      {"B c=4  io2 contiguous  order2", {L, 4, 12, 2, 0, 2, B, 8, 0}},
-      {"B c=4  io2 il4K        order1", {L, 4, 12, 2, 1, 1, B, 8, 0}},
       {"B c=4  io2 il1K        order1", {L, 4, 12, 2, 1, 1, B, 6, 0}},
-      {"B c=4  io2 il256       order1", {L, 4, 12, 2, 1, 1, B, 4, 0}},
-      {"B c=4  io2 il64K       order1", {L, 4, 12, 2, 1, 1, B, 12, 0}},
-      {"B c=4  io1 il256       order1", {L, 4, 12, 1, 1, 1, B, 4, 0}},
-      {"B c=4  io1 contiguous  order0", {L, 4, 12, 1, 0, 0, B, 8, 0}},
-      {"LC w0=6 read contiguous order0", {L, 4, 6, 2, 0, 0, B, 8, 1}},
-      {"LC w0=6 read il4K      order1", {L, 4, 6, 2, 1, 1, B, 8, 1}},
-      {"LC w0=6 read il256     order1", {L, 4, 6, 2, 1, 1, B, 4, 1}},
-      {"read A  contiguous      order0", {L, 12, 12, 2, 0, 0, B, 8, 1}},
-      {"read A  il4K            order1", {L, 12, 12, 2, 1, 1, B, 8, 1}},
+      {"LC c=4 w0=6 read il1K  order1", {L, 4, 6, 2, 1, 1, B, 6, 1}},
+      {"LC c=2 w0=5 read il1K  order1", {L, 2, 5, 2, 1, 1, B, 6, 1}},
+      {"LC c=2 w0=5 read il1K  order0", {L, 2, 5, 2, 1, 0, B, 6, 1}},
+      {"LC c=3 w0=5 read il1K  order1", {L, 3, 5, 2, 1, 1, B, 6, 1}},
   };
   const unsigned blocks = (unsigned)(n / 4096);
   for (auto& cs : cases) {
     const float ms = time_it([&] { hipLaunchKernelGGL(k_pass, dim3(blocks), dim3(256), 0, 0, a, cs.p, 0.0); }, 8);
     printf("%-34s %8.3f ms %7.0f GB/s\n", cs.name, ms, (cs.p.ro ? 1.0 : 2.0) * n * 16 / ms / 1e6);
     fflush(stdout);
+  }
+  {
+    // the 8-site group (sites 12..19) with 5 / 6 column bits
+    const float m1 = time_it([&] { hipLaunchKernelGGL((k_big<1>), dim3(blocks / 2), dim3(512), 0, 0, a, L, 5, 12, 0.0); }, 8);
+    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=5 8192-amp tiles (512 thr)", m1, 2.0 * n * 16 / m1 / 1e6);
+    const float m2 = time_it([&] { hipLaunchKernelGGL((k_big<2>), dim3(blocks / 4), dim3(1024), 0, 0, a, L, 6, 12, 0.0); }, 8);
+    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=6 16384-amp tiles (1024 thr)", m2, 2.0 * n * 16 / m2 / 1e6);
+    const float m0 = time_it([&] { hipLaunchKernelGGL((k_big<0>), dim3(blocks), dim3(256), 0, 0, a, L, 4, 12, 0.0); }, 8);
+    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=4 4096-amp tiles (k_big ref)", m0, 2.0 * n * 16 / m0 / 1e6);
   }
   return 0;
 }
