@@ -96,6 +96,7 @@ struct dtc_ctx {
   int octet_bits = 6;        // DTC_OCTET_BITS (0 = contiguous states)
   int lc_split = 1;          // DTC_LC_SPLIT
   int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
+  bool lc_wide = true;       // DTC_NO_LCW unset: five-pass (10-site) light-cone ends
   // DTC_KDK_SPLIT: which K-D-K passes run three workgroups per CU (dtc_kernels.h
   // PassArgs::kdk_split): the 12-site probe passes, every per-site/energy pass
   int kdk_split = (1 << 7) | (1 << (8 + 7)) | (1 << (8 + 6));
@@ -333,9 +334,19 @@ struct PassSpec {
   // sites of lc_mask (bit 8 l + b: site lc_w0 + b in layer l), then the probe
   int lc_w0 = -1;
   int lc_layers = 0;
-  KickDesc lc[dtc::kLcLayers] = {};
+  KickDesc lc[dtc::kLcMaxLayers] = {};
   uint64_t lc_mask = 0;
+  // the 10-site form (lc_merge_wide): tile bit k = global bit lc_gb[k], lc_mask
+  // bit 10 l + k - 2 = tile bit k kicked in layer l
+  int lc_wide = 0;
+  int8_t lc_gb[dtc::kTileBits] = {};
 };
+
+// the tile bits a light-cone pass kicks in layer l (nonzero: the layer runs)
+uint64_t lc_layer_bits(const PassSpec& ps, int l) {
+  return ps.lc_wide ? (ps.lc_mask >> (10 * l)) & 0x3FFull
+                    : (ps.lc_mask >> (dtc::kLcSites * l)) & 0xFFull;
+}
 
 // The tile geometry of a pass (the plan's group, or the light-cone window).
 Group pass_group(const Plan& pl, const PassSpec& ps) {
@@ -444,7 +455,7 @@ int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
   int kind = shape == dtc::kShapeD ? dtc::kKindRX : -1;
   std::vector<const KickDesc*> ks{&ps.pre, &ps.post};
   for (int l = 0; l < ps.lc_layers; ++l)
-    if ((ps.lc_mask >> (dtc::kLcSites * l)) & 0xFFull) ks.push_back(&ps.lc[l]);
+    if (lc_layer_bits(ps, l)) ks.push_back(&ps.lc[l]);
   for (const KickDesc* k : ks) {
     if (!k->enabled) continue;
     const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
@@ -464,8 +475,10 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
   pk.pre = ps.pre;
   pk.post = ps.post;
   pk.lc_layers = ps.lc_layers;
-  for (int l = 0; l < dtc::kLcLayers; ++l) pk.lc[l] = ps.lc[l];
+  for (int l = 0; l < dtc::kLcMaxLayers; ++l) pk.lc[l] = ps.lc[l];
   pk.lc_mask = ps.lc_mask;
+  pk.lc_wide = ps.lc_wide;
+  for (int k = 0; k < dtc::kTileBits; ++k) pk.lc_gb[k] = ps.lc_gb[k];
   pk.kind = pass_kind(rc, ps, pass_shape(ps));
   pk.c = g.c;
   pk.s = g.s;
@@ -563,6 +576,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.lc_layers = ps.lc_layers;
   A.lc_mask = ps.lc_mask;
   A.lc_diag = (const double2*)ctx->lc_diag.p;
+  A.lc_wide = ps.lc_wide;
+  for (int k = 0; k < dtc::kTileBits; ++k) A.lc_gb[k] = ps.lc_gb[k];
   A.batch = batch;
   A.n_obs = n_obs;
   const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
@@ -768,7 +783,9 @@ uint64_t init_state_mask(const RunCfg& rc, uint64_t traj) {
 
 // Cone diagonals of the light-cone pass (dtc_kernels.h, kLcTab): for r = 1..4
 // the terms of D on sites j-r+1 .. j+r-1 and every bond touching them, as a
-// function of bits lo..hi = j-r .. j+r (clipped to [0, L)).
+// function of bits lo..hi = j-r .. j+r (clipped to [0, L)); r = 5 split at j
+// into bits j-5 .. j (fields j-4 .. j, bonds from j-5) and j .. j+5 (fields
+// j+1 .. j+4, bonds from j to j+5).
 void build_cone_tables(int L, int j, int n_inst, const double* h, const double* phi,
                        std::vector<double>& out) {
   out.assign((size_t)n_inst * dtc::kLcTab * 2, 0.0);
@@ -780,6 +797,18 @@ void build_cone_tables(int L, int j, int n_inst, const double* h, const double* 
       double* o = out.data() + ((size_t)in * dtc::kLcTab + dtc::lc_tab_off(r)) * 2;
       for (int v = 0; v < (1 << (hi - lo + 1)); ++v) {
         const double ang = diag_angle(L, hh, pp, std::max(0, j - r + 1), j + r, j - r, j + r, lo, v);
+        o[2 * v] = std::cos(-0.5 * ang);
+        o[2 * v + 1] = std::sin(-0.5 * ang);
+      }
+    }
+    for (int part = 0; part < 2; ++part) {
+      const int lo = part == 0 ? std::max(0, j - 5) : j;
+      const int hi = part == 0 ? j : std::min(L - 1, j + 5);
+      double* o = out.data() + ((size_t)in * dtc::kLcTab + (part == 0 ? dtc::kLcTab5a : dtc::kLcTab5b)) * 2;
+      for (int v = 0; v < (1 << (hi - lo + 1)); ++v) {
+        const double ang = part == 0
+                               ? diag_angle(L, hh, pp, std::max(0, j - 4), j + 1, j - 5, j, lo, v)
+                               : diag_angle(L, hh, pp, j + 1, j + 5, j, j + 5, lo, v);
         o[2 * v] = std::cos(-0.5 * ang);
         o[2 * v + 1] = std::sin(-0.5 * ang);
       }
@@ -892,55 +921,123 @@ uint32_t skip_bits(const Group& g, uint64_t mask) {
   return sk;
 }
 
-// Light-cone end of the echo chain sched[chain0 ..) measuring Z_j: replace
-// its last k passes (k = 4 .. 2, the first that fits) by one kShapeLC pass.
-// The passes' kicks and diagonals, in order, form layers separated by the
-// D*'s; layer l of M (r = M - 1 - l diagonals before the probe) only matters
-// on sites j-r .. j+r, and the layers' remaining sites must fit one 8-site
-// window w0 .. w0+7 (4 <= w0 <= L - 8: clear of tile bits 0..3).
-void lc_merge(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j) {
+// The kick layers of a chain's last k passes, in order, separated by the
+// D*'s (a layer of one period spans two passes: the post-kick of one group and
+// the pre-kick of the next); trailing diagonals are dropped.  False when the
+// passes do not form such layers (not a D* chain, a light-cone pass already).
+bool lc_layers_of(const RunCfg& rc, const std::vector<Launch>& sched, int k,
+                  std::vector<KickDesc>& desc, std::vector<uint64_t>& sites) {
   const Plan& pl = rc.pl;
-  const int L = pl.L;
   auto same_layer = [](const KickDesc& a, const KickDesc& b) {
     return a.row == b.row && a.mode == b.mode && a.stream == b.stream &&
            a.rng_period == b.rng_period;
   };
+  desc.assign(1, no_kick());
+  sites.assign(1, 0);
+  bool ok = true;
+  int pending_d = 0;  // diagonals not yet followed by a kick (trailing ones are dropped)
+  auto kick = [&](const Group& g, const KickDesc& kd) {
+    for (; pending_d > 0; --pending_d) {
+      desc.push_back(no_kick());
+      sites.push_back(0);
+    }
+    if (desc.back().enabled && !same_layer(desc.back(), kd)) ok = false;
+    desc.back() = kd;
+    desc.back().skip = 0;
+    sites.back() |= layer_sites(g, kd, pl.L);
+  };
+  for (size_t i = sched.size() - k; i < sched.size(); ++i) {
+    const PassSpec& ps = sched[i].ps;
+    if (ps.lc_w0 >= 0) ok = false;
+    if (!ok) break;
+    const Group& g = pl.groups[ps.group];
+    if (ps.pre.enabled) kick(g, ps.pre);
+    if (ps.diag != dtc::kDiagNone) {
+      if (ps.diag != dtc::kDiagConj) ok = false;
+      ++pending_d;
+    }
+    if (ps.post.enabled) kick(g, ps.post);
+  }
+  return ok;
+}
+
+// The sites of j's cone (radius r), clipped to [0, L).
+uint64_t cone_sites(int L, int j, int r) {
+  uint64_t cone = 0;
+  for (int i = std::max(0, j - r); i <= std::min(L - 1, j + r); ++i) cone |= 1ull << i;
+  return cone;
+}
+
+// The 10-site light-cone end (dtc_lcw_final): the chain's last five passes
+// as six layers r = 5 .. 0 on the window j-5 .. j+4 or j-4 .. j+5 (the cone
+// of r = 4 plus the first layer's group), tile bits 0, 1 = global bits 0, 1.
+// The kernel's fixed nibble program needs layers r <= 1 on j-2 .. j+1 (nibble
+// 1), r <= 3 on nibbles 1 and 2 (+ j+2, j+3, j-4, j-3): checked here, as the
+// window's bounds; false leaves the chain to lc_merge's 8-site form.
+bool lc_merge_wide(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j) {
+  const Plan& pl = rc.pl;
+  const int L = pl.L;
+  if ((int)(sched.size() - chain0) < 5) return false;
+  if (j - 4 < 2 || j + 3 > L - 1) return false;
+  std::vector<KickDesc> desc;
+  std::vector<uint64_t> sites;
+  if (!lc_layers_of(rc, sched, 5, desc, sites) || (int)desc.size() != dtc::kLcwLayers) return false;
+  uint64_t u = 1ull << j;
+  for (int l = 0; l < dtc::kLcwLayers; ++l) {
+    sites[l] &= cone_sites(L, j, dtc::kLcwLayers - 1 - l);
+    u |= sites[l];
+  }
+  const uint64_t nib1 = 0xFull << (j - 2);
+  const uint64_t nib2 = (3ull << (j + 2)) | (3ull << (j - 4));
+  if ((sites[4] | sites[5]) & ~nib1) return false;
+  if ((sites[2] | sites[3]) & ~(nib1 | nib2)) return false;
+  uint64_t rest = u & ~(nib1 | nib2);
+  if (__builtin_popcountll(rest) > 2 || (rest & 3ull)) return false;
+  // the two low tile bits beside the columns: the outer sites, padded with
+  // free bits of the state (their kicks stay off)
+  for (int g = 2; g < pl.L_eff && __builtin_popcountll(rest) < 2; ++g)
+    if (!(((nib1 | nib2 | rest) >> g) & 1ull)) rest |= 1ull << g;
+  if (__builtin_popcountll(rest) != 2) return false;
+  PassSpec lc{sched.back().ps.group, no_kick(), no_kick(), dtc::kDiagConj, sched.back().ps.d_index};
+  const int r0 = __builtin_ctzll(rest), r1 = 63 - __builtin_clzll(rest);
+  const int gb[dtc::kTileBits] = {0, 1, r0, r1, j - 2, j - 1, j, j + 1, j + 2, j + 3, j - 4, j - 3};
+  lc.lc_w0 = j - 4;  // (marks the light-cone pass; the tile is lc_gb)
+  lc.lc_wide = 1;
+  lc.lc_layers = dtc::kLcwLayers;
+  for (int k = 0; k < dtc::kTileBits; ++k) lc.lc_gb[k] = (int8_t)gb[k];
+  for (int l = 0; l < dtc::kLcwLayers; ++l) {
+    lc.lc[l] = desc[l];
+    for (int k = 2; k < dtc::kTileBits; ++k)
+      if ((sites[l] >> gb[k]) & 1ull) lc.lc_mask |= 1ull << (10 * l + k - 2);
+  }
+  const int kind = pass_kind(rc, lc, dtc::kShapeLC);
+  if (kind != dtc::kKindRX && kind != dtc::kKindRY) return false;
+  const Launch first = sched[sched.size() - 5];
+  sched.resize(sched.size() - 5 + 1);
+  sched.back() = Launch{lc, first.src, first.dst, dtc::kMeasProbe, 1, 2, nullptr, first.meas_stride};
+  return true;
+}
+
+// Light-cone end of the echo chain sched[chain0 ..) measuring Z_j: replace
+// its last k passes by one kShapeLC pass -- five (lc_merge_wide, when enabled
+// and it fits), else k = 4 .. 2 (the first that fits) over an 8-site window.
+// Layer l of M (r = M - 1 - l diagonals before the probe) only matters on
+// sites j-r .. j+r, and the layers' remaining sites must fit the window
+// w0 .. w0+7 (4 <= w0 <= L - 8: clear of tile bits 0..3).
+void lc_merge(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j, bool wide) {
+  const Plan& pl = rc.pl;
+  const int L = pl.L;
+  if (wide && lc_merge_wide(rc, sched, chain0, j)) return;
   const int n_chain = (int)(sched.size() - chain0);
   for (int k = std::min(4, n_chain); k >= 2; --k) {
-    std::vector<KickDesc> desc(1, no_kick());
-    std::vector<uint64_t> sites(1, 0);
-    bool ok = true;
-    int pending_d = 0;  // diagonals not yet followed by a kick (trailing ones are dropped)
-    auto kick = [&](const Group& g, const KickDesc& kd) {
-      for (; pending_d > 0; --pending_d) {
-        desc.push_back(no_kick());
-        sites.push_back(0);
-      }
-      if (desc.back().enabled && !same_layer(desc.back(), kd)) ok = false;
-      desc.back() = kd;
-      desc.back().skip = 0;
-      sites.back() |= layer_sites(g, kd, L);
-    };
-    for (size_t i = sched.size() - k; i < sched.size(); ++i) {
-      const PassSpec& ps = sched[i].ps;
-      if (ps.lc_w0 >= 0) ok = false;
-      if (!ok) break;
-      const Group& g = pl.groups[ps.group];
-      if (ps.pre.enabled) kick(g, ps.pre);
-      if (ps.diag != dtc::kDiagNone) {
-        if (ps.diag != dtc::kDiagConj) ok = false;
-        ++pending_d;
-      }
-      if (ps.post.enabled) kick(g, ps.post);
-    }
+    std::vector<KickDesc> desc;
+    std::vector<uint64_t> sites;
+    const bool ok = lc_layers_of(rc, sched, k, desc, sites);
     const int M = (int)desc.size();
     if (!ok || M > dtc::kLcLayers) continue;
     uint64_t u = 1ull << j;
     for (int l = 0; l < M; ++l) {
-      const int r = M - 1 - l;
-      uint64_t cone = 0;
-      for (int i = std::max(0, j - r); i <= std::min(L - 1, j + r); ++i) cone |= 1ull << i;
-      sites[l] &= cone;
+      sites[l] &= cone_sites(L, j, M - 1 - l);
       u |= sites[l];
     }
     const int lo = __builtin_ctzll(u), hi = 63 - __builtin_clzll(u);
@@ -991,6 +1088,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   if (const char* e = std::getenv("DTC_KDK_SPLIT")) c->kdk_split = std::atoi(e);
   c->basis_synth = std::getenv("DTC_NO_BASIS_SYNTH") == nullptr;
   c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
+  c->lc_wide = std::getenv("DTC_NO_LCW") == nullptr;
   if (const char* e = std::getenv("DTC_BATCH_BYTES")) c->batch_bytes = std::atof(e);
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1346,7 +1444,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         // of the kicks left: their layers, restricted to the cone, with D*
         // between them, then the probe.
         if (!rc.device && lc_enabled && sched.size() - chain0 >= 2)
-          lc_merge(rc, sched, chain0, pr->probe_site);
+          lc_merge(rc, sched, chain0, pr->probe_site, ctx->lc_wide);
         sched.back().meas_mode = dtc::kMeasProbe;
         sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;
         // the echo state is only measured: the chain's last pass reads its

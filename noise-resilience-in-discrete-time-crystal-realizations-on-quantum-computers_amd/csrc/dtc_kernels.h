@@ -72,8 +72,29 @@ static constexpr int kLcPacked = kLcCoefs + 1;
 // sites j-r+1 .. j+r-1 (r = M - 1 - l; the terms elsewhere commute with
 // everything after it), a function of bits j-r .. j+r (clipped to [0, L)):
 // per instance one table per r = 1 .. 4 at offset (2^(2r+1) - 8) / 3.
-static constexpr int kLcTab = 680;
+static constexpr int kLcTab4 = 680;  // the r = 1 .. 4 tables (what the 8-site pass stages)
 __host__ __device__ constexpr int lc_tab_off(int r) { return ((1 << (2 * r + 1)) - 8) / 3; }
+// The 10-site pass (kShapeLC with lc_wide) also needs r = 5, a function of 11
+// bits: split at j into two 6-bit tables, bits j-5 .. j (fields j-4 .. j,
+// bonds (j-5, j-4) .. (j-1, j)) and bits j .. j+5 (fields j+1 .. j+4, bonds
+// (j, j+1) .. (j+4, j+5)), clipped to [0, L): two lookups instead of a
+// 2048-entry table (which would leave LDS for two workgroups per CU only).
+static constexpr int kLcTab5a = kLcTab4;
+static constexpr int kLcTab5b = kLcTab4 + 64;
+static constexpr int kLcTab = kLcTab4 + 128;  // per-instance stride of PassArgs::lc_diag
+// kShapeLC with lc_wide: six kick layers over a 10-site window (one more
+// pass of the echo chain merged).  Tile bits 0, 1 = global bits 0, 1 (64-B
+// runs), tile bits 2 .. 11 = window sites lc_gb[2 .. 11] (host-chosen: nibble
+// 1 = j-2 .. j+1, nibble 2 = j+2, j+3, j-4, j-3, bits 2, 3 = the other two),
+// so the cone's inner layers stay in one or two register nibbles.  lc_mask
+// bit 10 l + k - 2 = tile bit k kicked in layer l.  Records (doubles): f^ of
+// (layer l, tile bit k) at 12 l + k; kLcwG2: prod w^2; kLcwMask + l (as
+// integer): the frame's X mask after layer l in global bit positions
+// (l = 5: the final one, for the probe's sign).
+static constexpr int kLcwLayers = 6;
+static constexpr int kLcwG2 = 12 * kLcwLayers;
+static constexpr int kLcwMask = kLcwG2 + 1;
+static constexpr int kLcMaxLayers = kLcwLayers;
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
@@ -122,8 +143,10 @@ struct PassKick {
   int kind;             // KickKind of the pass
   int c, s, act;        // tile geometry (see PassArgs)
   int lc_layers;        // kShapeLC: layers lc[0 .. lc_layers), site b of layer l kicked
-  KickDesc lc[kLcLayers];  // when bit 8 l + b of lc_mask is set (window site b = tile
+  KickDesc lc[kLcMaxLayers];  // when bit 8 l + b of lc_mask is set (window site b = tile
   uint64_t lc_mask;     // bit 4 + b); Pauli-frame records (kLcCoefs ..)
+  int lc_wide;          // the 10-site form: lc_mask bit 10 l + k - 2 = tile bit k of
+  int8_t lc_gb[kTileBits];  // layer l, tile bit k = global bit lc_gb[k] (kLcw* records)
 };
 
 struct PrepArgs {
@@ -188,6 +211,8 @@ struct PassArgs {
   int lc_layers;           // kShapeLC: kick layers; lc_mask bit 8 l + b = site b of layer l
   uint64_t lc_mask;
   const double2* lc_diag;  // kShapeLC: cone diagonals, [n_inst][kLcTab]
+  int lc_wide;             // kShapeLC: the 10-site form (dtc_lcw_final), tile bit k =
+  int8_t lc_gb[kTileBits]; // global bit lc_gb[k]
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]

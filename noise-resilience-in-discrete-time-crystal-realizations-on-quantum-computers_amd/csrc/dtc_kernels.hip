@@ -254,6 +254,42 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   const int64_t gstate = P.batch_start + b;
   const uint64_t traj = (uint64_t)(P.traj_offset + (gstate % P.n_traj));
   KickRec* out = P.out + id * kRecPerState;
+  if (pk.lc_layers > 0 && pk.lc_wide) {
+    // 10-site light-cone pass: the same Pauli frame over tile bits 2 .. 11
+    // (dtc_kernels.h, kLcw*); the X masks in global bit positions
+    double* od = (double*)out;
+    long long* oi = (long long*)out;
+    int fz = 0, fx = 0;  // per tile bit
+    double g2 = 1.0;
+    for (int l = 0; l < kLcwLayers; ++l) {
+      for (int k = 0; k < kTileBits; ++k) {
+        double fh = 0.0;
+        if (k >= 2 && l < pk.lc_layers && ((pk.lc_mask >> (10 * l + k - 2)) & 1ull)) {
+          const int lsite = pk.lc_gb[k];
+          double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0),
+                          make_double2(0.0, 0.0), make_double2(1.0, 0.0)};
+          if (lsite < P.L_real)
+            build_site_kick(P, pk.lc[l], P.site_of ? P.site_of[lsite] : lsite, traj, m);
+          SiteMat sm;
+          canonicalise(pk.kind, m, sm);
+          const int form_b = sm.var >> 1, neg = sm.var & 1;
+          const double ft = form_b ? -sm.coef : sm.coef;
+          const int flip = ((pk.kind == kKindRX ? fz : (fz ^ fx)) >> k) & 1;
+          fh = flip ? -ft : ft;
+          fz ^= (pk.kind == kKindRX ? neg : (neg ^ form_b)) << k;
+          fx ^= form_b << k;
+          g2 *= sm.scale * sm.scale;
+        }
+        od[12 * l + k] = fh;
+      }
+      long long mg = 0;
+      for (int k = 2; k < kTileBits; ++k)
+        if ((fx >> k) & 1) mg |= 1ll << pk.lc_gb[k];
+      oi[kLcwMask + l] = mg;
+    }
+    od[kLcwG2] = g2;
+    return;
+  }
   if (pk.lc_layers > 0) {
     // light-cone pass: Pauli-frame records (dtc_kernels.h, kLcCoefs ..)
     double* od = (double*)out;
@@ -1325,7 +1361,7 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
   __shared__ double2 s_tile[SPLIT ? 1 : kTile];
   __shared__ double s_half[SPLIT ? kTile : 1];
-  __shared__ double2 s_cone[kLcTab];
+  __shared__ double2 s_cone[kLcTab4];
   __shared__ double s_red[kThreads / 64][2];
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;  // c = 4, s = w0
@@ -1355,13 +1391,13 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
     return ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
   };
   M.tbase = tbase_of(tile0);
-  constexpr int kConePerThread = (kLcTab + kThreads - 1) / kThreads;
+  constexpr int kConePerThread = (kLcTab4 + kThreads - 1) / kThreads;
   double2 cv[kConePerThread];
   const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
 #pragma unroll
   for (int j = 0; j < kConePerThread; ++j) {
     const int i = t + j * kThreads;
-    if (i < kLcTab) cv[j] = ct[i];
+    if (i < kLcTab4) cv[j] = ct[i];
   }
   // the tile in layout 2 (threads = tile bits 0..7: 16-amplitude runs)
   // (layout 2: lanes = tile bits 0..3 (columns) and window sites 0..3; a
@@ -1383,7 +1419,7 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
 #pragma unroll
   for (int j = 0; j < kConePerThread; ++j) {
     const int i = t + j * kThreads;
-    if (i < kLcTab) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
+    if (i < kLcTab4) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
   }
   // (visible after the first re-layout's barrier)
   const double g2 = R.d(0, kLcG2);
@@ -1523,6 +1559,206 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lc_final_split(PassArgs A) {
   lc_body<KIND, 1, true>(A);
 }
 
+// ---- the 10-site light-cone end (kShapeLC, lc_wide) ------------------------
+// The chain's last five passes as six kick layers (r = 5 .. 0 diagonals before
+// the probe) on a 10-site window (dtc_kernels.h, kLcw*).  Tile bits 0, 1 =
+// global bits 0, 1 (64-B runs), tile bit k >= 2 = site lc_gb[k]: nibble 1 =
+// j-2 .. j+1 (the cone of r <= 1), nibble 2 = j+2, j+3, j-4, j-3 (with nibble
+// 1, r <= 3), nibble 0 = the columns and the two outer sites.  Program (the
+// nibble in registers; the host checks every layer's sites against it):
+//   r=5: 2 1 0 | D5 | r=4: 0 2 1 | D4 | r=3: 1 2 | D3 | r=2: 2 1 | D2 |
+//   r=1: 1 | D1 | r=0: 1 | probe (j = tile bit 6 = register bit 2)
+// — six re-layouts through the 32 KiB half-tile buffer for five passes (the
+// 8-site pass: five for four), three workgroups per CU.  D5 is two lookups
+// in the split radius-5 tables.  Global indices fit 32 bits (L_eff <= 32).
+template <int KIND>
+__global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
+  static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
+  __shared__ double s_half[kTile];
+  __shared__ double2 s_cone[kLcTab];
+  __shared__ double s_red[kThreads / 64][2];
+  const int t = threadIdx.x;
+  const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
+  const int og = A.octet_bits;
+  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
+  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  if (og && b >= A.batch) return;
+  const int inst = (int)((A.batch_start + b) / A.n_traj);
+  RecRegs R;
+  {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < kLcwMask + kLcwLayers) {  // the records: lanes 0 .. 19
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
+  constexpr int kConePerThread = (kLcTab + kThreads - 1) / kThreads;
+  double2 cv[kConePerThread];
+  const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
+#pragma unroll
+  for (int j = 0; j < kConePerThread; ++j) {
+    const int i = t + j * kThreads;
+    if (i < kLcTab) cv[j] = ct[i];
+  }
+  // tile bit -> global bit (wave-uniform), the window, the tile's base: the
+  // tile id's bits deposited, in order, into the global bits off the window
+  uint32_t gbit[kTileBits];
+  uint32_t win = 0;
+#pragma unroll
+  for (int k = 0; k < kTileBits; ++k) {
+    gbit[k] = 1u << A.lc_gb[k];
+    win |= gbit[k];
+  }
+  uint32_t tbase = 0;
+  {
+    uint32_t rest = (uint32_t)tile;
+    for (int g = 0; g < A.L_eff; ++g) {
+      if ((win >> g) & 1u) continue;
+      tbase |= (rest & 1u) << g;
+      rest >>= 1;
+    }
+  }
+  // the thread's part of the global index in layout LAY (register bits zero)
+  auto lane_part = [&](auto lay_tag) -> uint32_t {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int y = ybase<LAY>(t);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < kTileBits; ++k)
+      if (k < 4 * LAY || k >= 4 * LAY + 4) x |= ((y >> k) & 1) ? gbit[k] : 0u;
+    return x;
+  };
+  using L0 = std::integral_constant<int, 0>;
+  using L1 = std::integral_constant<int, 1>;
+  using L2 = std::integral_constant<int, 2>;
+  // register r's part in layout LAY (uniform)
+  auto reg_part = [&](auto lay_tag, int r) -> uint32_t {
+    constexpr int LAY = decltype(lay_tag)::value;
+    return ((r & 1) ? gbit[4 * LAY] : 0u) | ((r & 2) ? gbit[4 * LAY + 1] : 0u) |
+           ((r & 4) ? gbit[4 * LAY + 2] : 0u) | ((r & 8) ? gbit[4 * LAY + 3] : 0u);
+  };
+  // the tile in layout 2 (threads = tile bits 0 .. 7: the columns in lane bits 0, 1)
+  double2 v[kRegs];
+  {
+    const int64_t vofs = octet_spread((int64_t)lane_part(L2{}), og) << 4;
+    const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const char* a = src + (octet_spread((int64_t)(tbase | reg_part(L2{}, r)), og) << 4) + vofs;
+      const d2v w = __builtin_nontemporal_load((const d2v*)a);
+      v[r] = make_double2(w.x, w.y);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // records and tables landed, the tile's 16 loads in flight
+  const double cs = A.diag_conj ? -1.0 : 1.0;
+#pragma unroll
+  for (int j = 0; j < kConePerThread; ++j) {
+    const int i = t + j * kThreads;
+    if (i < kLcTab) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
+  }
+  // (visible after the first re-layout's barrier)
+  const int jp = A.probe;
+  const int Lr = A.L_real;
+
+  // kicks of layer l on the kicked sites of nibble N (in registers)
+  auto kick = [&](auto n_tag, auto l_tag) {
+    constexpr int N = decltype(n_tag)::value;
+    constexpr int l = decltype(l_tag)::value;
+    const uint32_t m = (uint32_t)(A.lc_mask >> (10 * l));
+    if constexpr (4 * N + 0 >= 2)
+      if ((m >> (4 * N + 0 - 2)) & 1u) layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
+    if constexpr (4 * N + 1 >= 2)
+      if ((m >> (4 * N + 1 - 2)) & 1u) layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
+    if ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
+    if ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
+  };
+  // one cone-table factor in layout LAY: tab[((x ^ m) >> lo) & msk] per amplitude
+  auto diag_tab = [&](auto lay_tag, uint32_t xm, int lo, int hi, const double2* tab) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const uint32_t msk = (1u << (hi - lo + 1)) - 1u;
+    const int base = (int)((xm >> lo) & msk);
+    const int o0 = (int)((gbit[4 * LAY] >> lo) & msk), o1 = (int)((gbit[4 * LAY + 1] >> lo) & msk);
+    const int o2 = (int)((gbit[4 * LAY + 2] >> lo) & msk), o3 = (int)((gbit[4 * LAY + 3] >> lo) & msk);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const int off = ((r & 1) ? o0 : 0) ^ ((r & 2) ? o1 : 0) ^ ((r & 4) ? o2 : 0) ^ ((r & 8) ? o3 : 0);
+      v[r] = cmul(v[r], tab[base ^ off]);
+    }
+  };
+  // the cone diagonal after layer l (r = 5 - l), frame X mask m_l
+  auto diag = [&](auto lay_tag, auto l_tag) {
+    constexpr int l = decltype(l_tag)::value;
+    constexpr int rad = kLcwLayers - 1 - l;
+    const uint32_t xm = (tbase | lane_part(lay_tag)) ^ (uint32_t)R.bits(kLcwMask + l);
+    if constexpr (rad == 5) {
+      diag_tab(lay_tag, xm, max(0, jp - 5), jp, s_cone + kLcTab5a);
+      diag_tab(lay_tag, xm, jp, min(Lr - 1, jp + 5), s_cone + kLcTab5b);
+    } else {
+      diag_tab(lay_tag, xm, max(0, jp - rad), min(Lr - 1, jp + rad), s_cone + lc_tab_off(rad));
+    }
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+  using C3 = std::integral_constant<int, 3>;
+  using C4 = std::integral_constant<int, 4>;
+  using C5 = std::integral_constant<int, 5>;
+  // r = 5: nibbles 2, 1, 0
+  kick(L2{}, C0{});
+  exchange_split<2, 1>(v, s_half, t);
+  kick(L1{}, C0{});
+  exchange_split<1, 0>(v, s_half, t);
+  kick(L0{}, C0{});
+  diag(L0{}, C0{});
+  // r = 4: nibbles 0, 2, 1
+  kick(L0{}, C1{});
+  exchange_split<0, 2>(v, s_half, t);
+  kick(L2{}, C1{});
+  exchange_split<2, 1>(v, s_half, t);
+  kick(L1{}, C1{});
+  diag(L1{}, C1{});
+  // r = 3: nibbles 1, 2
+  kick(L1{}, C2{});
+  exchange_split<1, 2>(v, s_half, t);
+  kick(L2{}, C2{});
+  diag(L2{}, C2{});
+  // r = 2: nibbles 2, 1
+  kick(L2{}, C3{});
+  exchange_split<2, 1>(v, s_half, t);
+  kick(L1{}, C3{});
+  diag(L1{}, C3{});
+  // r = 1, r = 0: nibble 1
+  kick(L1{}, C4{});
+  diag(L1{}, C4{});
+  kick(L1{}, C5{});
+  // probe: j at register bit 2 of layout 1; the frame's final X on j flips it
+  double ptot = 0.0, pz = 0.0;
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+    ptot += p2;
+    pz += ((r >> 2) & 1) ? -p2 : p2;
+  }
+  if ((R.bits(kLcwMask + kLcwLayers - 1) >> jp) & 1) pz = -pz;
+  const double g2 = R.d(0, kLcwG2);
+  const int wave = t >> 6, lane = t & 63;
+  const double tot = wave_sum(ptot) * g2;
+  const double z = wave_sum(pz) * g2;
+  if (lane == 0) {
+    s_red[wave][0] = tot;
+    s_red[wave][1] = z;
+  }
+  __syncthreads();
+  if (t < 2) {
+    double acc = 0.0;
+    for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
+    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+  }
+}
+
 template <int NIBS, int KIND, int MC>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
@@ -1610,6 +1846,22 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
     return hipErrorInvalidValue;
   // octet layout: the eight states of an octet on consecutive blocks
   dim3 grid = a.octet_bits ? dim3(n_tiles * 8, (batch + 7) / 8) : dim3(n_tiles, batch);
+  if (shape == kShapeLC && a.lc_wide) {
+    // 10-site light-cone pass: six layers, tile bits 0, 1 = global 0, 1, the
+    // probe at tile bit 6, twelve distinct global bits inside the state
+    if (a.meas != kMeasProbe || !a.no_store || a.lc_layers != kLcwLayers || a.n_obs < 2 ||
+        !a.lc_diag || a.lc_gb[0] != 0 || a.lc_gb[1] != 1 || a.lc_gb[6] != a.probe ||
+        (kind != kKindRX && kind != kKindRY))
+      return hipErrorInvalidValue;
+    uint64_t seen = 0;
+    for (int k = 0; k < kTileBits; ++k) {
+      if (a.lc_gb[k] < 0 || a.lc_gb[k] >= a.L_eff || ((seen >> a.lc_gb[k]) & 1)) return hipErrorInvalidValue;
+      seen |= 1ull << a.lc_gb[k];
+    }
+    hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX> : dtc_lcw_final<kKindRY>), grid,
+                       dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+  }
   if (shape == kShapeLC) {
     // measure-only light-cone pass: probe, window at tile bits 4..11 (c = 4)
     if (a.c != 4 || a.act != 0xFF0 || a.meas != kMeasProbe || !a.no_store || a.lc_layers < 1 ||

@@ -205,23 +205,45 @@ def test_noise_sampler_unbiased_high_resolution(pkg, engine):
     (18, 6, 0.1, "vacuum", "x", 1, 13),
     (22, 8, 0.05, "vacuum", "y", 0, None),
 ])
-def test_echo_light_cone_end(pkg, engine, monkeypatch, L, T, p, state, pol, toff, probe):
+def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe):
     """Echo chains ending in the light-cone pass (the chain's last passes merged
-    into one measure-only pass over an 8-site window, each kick layer cut to the
-    light cone of Z_j): the same per-trajectory echo as the oracle (1e-10) and
-    as the engine without the merge (DTC_NO_LIGHTCONE=1)."""
+    into one measure-only pass, each kick layer cut to the light cone of Z_j):
+    five passes over a 10-site window (dtc_lcw_final) where it fits, else four
+    over an 8-site window (DTC_NO_LCW=1 forces the latter everywhere).  Both
+    give the same per-trajectory echo as the oracle (1e-10) and as the engine
+    without the merge (DTC_NO_LIGHTCONE=1).  The options are read when an
+    engine opens, so each variant runs on its own engine."""
     rng = np.random.default_rng(L * 31 + T)
     hs, phis = random_disorder(rng, L, 2)
     kw = {} if probe is None else {"probe_site": probe}
     spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
                          initial_state=state, t_offset=toff, **kw)
-    got = engine.autocorr(spec, 3, seed=77)
+
+    def run(env):
+        with monkeypatch.context() as m:
+            for k in env:
+                m.setenv(k, "1")
+            with pkg.DtcEngine(0) as eng:
+                eng.set_profiling(True)
+                out = eng.autocorr(spec, 3, seed=77)
+                st = eng.kernel_stats()
+        return out, st[pkg._capi.KERNEL_LO_PASS]["launches"] + st[pkg._capi.KERNEL_HI_PASS]["launches"]
+
+    got, n_wide = run([])
     ref = c_oracle.autocorr(spec, 3, seed=77)
     _cmp(got, ref)
-    monkeypatch.setenv("DTC_NO_LIGHTCONE", "1")
-    full = engine.autocorr(spec, 3, seed=77)
-    assert np.abs(got["echo"] - full["echo"]).max() < 1e-12
-    assert np.abs(got["fwd"] - full["fwd"]).max() == 0.0
+    narrow, n_narrow = run(["DTC_NO_LCW"])
+    full, n_full = run(["DTC_NO_LIGHTCONE"])
+    for o in (narrow, full):
+        assert np.abs(got["echo"] - o["echo"]).max() < 1e-12
+        assert np.abs(got["fwd"] - o["fwd"]).max() == 0.0
+    assert n_wide <= n_narrow <= n_full
+    if pol in ("x", "y"):  # factored kicks (general 2x2 kicks keep the full passes)
+        assert n_narrow < n_full
+        j = spec.probe_site
+        # two site groups (L <= 21: five passes = six layers), the window inside
+        if j - 4 >= 2 and j + 3 <= L - 1 and T >= 6 and L <= 21:
+            assert n_wide < n_narrow  # the 10-site window merged a fifth pass somewhere
 
 
 def test_independent_t_matches_oracle(pkg, engine):
