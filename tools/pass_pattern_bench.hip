@@ -34,8 +34,22 @@
 typedef double d2v __attribute__((ext_vector_type(2)));
 
 struct Pat {
-  int L, c, s, io, layout, order, batch, gbits, ro;
+  int L, c, s, io, layout, order, batch, gbits, ro, sw;
 };
+
+// state-index swizzles (bijective: high source bits XORed into disjoint low
+// target bits), applied before the state layout (round 3, r3u)
+__device__ __forceinline__ int64_t swz(int sw, int64_t x) {
+  switch (sw) {
+    case 1: return x ^ (((x >> 12) & 3) << 4);      // rows 12, 13 -> column quarter bits 4, 5
+    case 2: return x ^ (((x >> 12) & 7) << 6);      // rows 12..14 -> 1 KiB run bits 6..8
+    case 3: return x ^ (((x >> 12) & 15) << 4);     // rows 12..15 -> bits 4..7
+    case 4: return x ^ (((x >> 12) & 255) << 4);    // rows 12..19 -> bits 4..11
+    case 5: return x ^ (((x >> 16) & 15) << 6);     // rows 16..19 -> bits 6..9
+    case 6: return x ^ (((x >> 12) & 63) << 6);     // rows 12..17 -> bits 6..11
+    default: return x;
+  }
+}
 
 // layout 1: octets of states interleaved at 2^gbits amplitudes
 __device__ __forceinline__ int64_t addr_of(const Pat& P, int64_t st, int64_t x) {
@@ -89,7 +103,7 @@ __global__ __launch_bounds__(256, 2) void k_pass(d2v* __restrict__ a, Pat P, dou
   };
   d2v v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = __builtin_nontemporal_load(&a[addr_of(P, st, tbase | rel(ty(r)))]);
+  for (int r = 0; r < 16; ++r) v[r] = __builtin_nontemporal_load(&a[addr_of(P, st, swz(P.sw, tbase | rel(ty(r))))]);
   if (f == 12345.0) s_pad[t] = v[0];
   if (P.ro) {  // read only (the light-cone pass)
     d2v acc = v[0];
@@ -100,7 +114,7 @@ __global__ __launch_bounds__(256, 2) void k_pass(d2v* __restrict__ a, Pat P, dou
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r)
-    __builtin_nontemporal_store(v[r] * (1.0 + f), &a[addr_of(P, st, tbase | rel(ty(r)))]);
+    __builtin_nontemporal_store(v[r] * (1.0 + f), &a[addr_of(P, st, swz(P.sw, tbase | rel(ty(r))))]);
 }
 
 // Larger tiles for the 8-site group: 2^(12+E) amplitudes = c column bits +
@@ -159,27 +173,33 @@ int main() {
     const char* name;
     Pat p;
   } cases[] = {
-      {"A c=12 io1 il1K        order1", {L, 12, 12, 1, 1, 1, B, 6, 0}},
-      {"B c=4  io2 il1K        order1", {L, 4, 12, 2, 1, 1, B, 6, 0}},
-      {"LC c=4 w0=6 read il1K  order1", {L, 4, 6, 2, 1, 1, B, 6, 1}},
-      {"LC c=2 w0=5 read il1K  order1", {L, 2, 5, 2, 1, 1, B, 6, 1}},
-      {"LC c=2 w0=5 read il1K  order0", {L, 2, 5, 2, 1, 0, B, 6, 1}},
-      {"LC c=3 w0=5 read il1K  order1", {L, 3, 5, 2, 1, 1, B, 6, 1}},
+      {"A c=12 io1 il1K order1 sw0", {L, 12, 12, 1, 1, 1, B, 6, 0, 0}},
+      {"B c=4  io2 il1K order1 sw0", {L, 4, 12, 2, 1, 1, B, 6, 0, 0}},
+      {"A c=12 io1 il1K order1 sw1", {L, 12, 12, 1, 1, 1, B, 6, 0, 1}},
+      {"B c=4  io2 il1K order1 sw1", {L, 4, 12, 2, 1, 1, B, 6, 0, 1}},
+      {"A c=12 io1 il1K order1 sw2", {L, 12, 12, 1, 1, 1, B, 6, 0, 2}},
+      {"B c=4  io2 il1K order1 sw2", {L, 4, 12, 2, 1, 1, B, 6, 0, 2}},
+      {"A c=12 io1 il1K order1 sw3", {L, 12, 12, 1, 1, 1, B, 6, 0, 3}},
+      {"B c=4  io2 il1K order1 sw3", {L, 4, 12, 2, 1, 1, B, 6, 0, 3}},
+      {"A c=12 io1 il1K order1 sw4", {L, 12, 12, 1, 1, 1, B, 6, 0, 4}},
+      {"B c=4  io2 il1K order1 sw4", {L, 4, 12, 2, 1, 1, B, 6, 0, 4}},
+      {"A c=12 io1 il1K order1 sw5", {L, 12, 12, 1, 1, 1, B, 6, 0, 5}},
+      {"B c=4  io2 il1K order1 sw5", {L, 4, 12, 2, 1, 1, B, 6, 0, 5}},
+      {"A c=12 io1 il1K order1 sw6", {L, 12, 12, 1, 1, 1, B, 6, 0, 6}},
+      {"B c=4  io2 il1K order1 sw6", {L, 4, 12, 2, 1, 1, B, 6, 0, 6}},
+      {"B c=4  io2 il256 order1 sw0", {L, 4, 12, 2, 1, 1, B, 4, 0, 0}},
+      {"B c=4  io2 il256 order1 sw4", {L, 4, 12, 2, 1, 1, B, 4, 0, 4}},
+      {"A c=12 io1 il4K order1 sw4", {L, 12, 12, 1, 1, 1, B, 8, 0, 4}},
+      {"B c=4  io2 il4K order1 sw4", {L, 4, 12, 2, 1, 1, B, 8, 0, 4}},
+      {"B c=4  io2 il4K order1 sw6", {L, 4, 12, 2, 1, 1, B, 8, 0, 6}},
+      {"A c=12 io1 il1K order1 sw0 (again)", {L, 12, 12, 1, 1, 1, B, 6, 0, 0}},
+      {"B c=4  io2 il1K order1 sw0 (again)", {L, 4, 12, 2, 1, 1, B, 6, 0, 0}},
   };
   const unsigned blocks = (unsigned)(n / 4096);
   for (auto& cs : cases) {
     const float ms = time_it([&] { hipLaunchKernelGGL(k_pass, dim3(blocks), dim3(256), 0, 0, a, cs.p, 0.0); }, 8);
     printf("%-34s %8.3f ms %7.0f GB/s\n", cs.name, ms, (cs.p.ro ? 1.0 : 2.0) * n * 16 / ms / 1e6);
     fflush(stdout);
-  }
-  {
-    // the 8-site group (sites 12..19) with 5 / 6 column bits
-    const float m1 = time_it([&] { hipLaunchKernelGGL((k_big<1>), dim3(blocks / 2), dim3(512), 0, 0, a, L, 5, 12, 0.0); }, 8);
-    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=5 8192-amp tiles (512 thr)", m1, 2.0 * n * 16 / m1 / 1e6);
-    const float m2 = time_it([&] { hipLaunchKernelGGL((k_big<2>), dim3(blocks / 4), dim3(1024), 0, 0, a, L, 6, 12, 0.0); }, 8);
-    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=6 16384-amp tiles (1024 thr)", m2, 2.0 * n * 16 / m2 / 1e6);
-    const float m0 = time_it([&] { hipLaunchKernelGGL((k_big<0>), dim3(blocks), dim3(256), 0, 0, a, L, 4, 12, 0.0); }, 8);
-    printf("%-34s %8.3f ms %7.0f GB/s\n", "B c=4 4096-amp tiles (k_big ref)", m0, 2.0 * n * 16 / m0 / 1e6);
   }
   return 0;
 }

@@ -22,9 +22,10 @@ def main(prof, out, batch, L, bench_args=""):
            "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 FETCH_SIZE halving"}
     amps = float(1 << max(L, 12)) * batch
     for kname, key in (("dtc_kdk_pass", "lo_pass"), ("dtc_kick_pass", "hi_pass"),
-                       ("dtc_lc_final", "lightcone_pass")):
-        fsel = fe[fe.Kernel_Name.str.contains(kname)]["Counter_Value"]
-        wsel = wr[wr.Kernel_Name.str.contains(kname)]["Counter_Value"]
+                       ("dtc_lc_final", "lightcone_pass"),
+                       ("dtc_lcw_final", "lightcone_wide_pass")):
+        fsel = fe[fe.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
+        wsel = wr[wr.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
         if not len(fsel) or not len(wsel):
             continue
         f = fsel.mean() * 1024
