@@ -460,10 +460,16 @@ int pass_kind(const RunCfg& rc, const PassSpec& ps, int shape) {
     if (!k->enabled) continue;
     const bool basis_x = k->mode == dtc::kKickBasisX || k->mode == dtc::kKickUndoBasisX;
     int rk = basis_x ? dtc::kKindGen : rc.row_kind[k->row];
-    // device-like noise: Kraus x Pauli x gate is not unitary, but stays in
-    // the RX / RY family: the unfactored butterflies
-    if (rc.device && rk == dtc::kKindRX) rk = dtc::kKindRXU;
-    if (rc.device && rk == dtc::kKindRY) rk = dtc::kKindRYU;
+    // device-like noise: Kraus x Pauli x gate is not unitary; with one
+    // sub-gate per kick it is a real diagonal times a unitary of the family
+    // (SiteMat in dtc_kernels.hip: factored, the diagonal deferred); Kraus
+    // factors between sub-gates, or a dagger (undo) putting the diagonal on
+    // the right, leave only the general form
+    if (rc.device && (rk == dtc::kKindRX || rk == dtc::kKindRY)) {
+      const bool left_diag = rc.prob->n_sub == 1 && k->mode != dtc::kKickUndo &&
+                             k->mode != dtc::kKickUndoBasisX;
+      rk = !left_diag ? dtc::kKindGen : (rk == dtc::kKindRX ? dtc::kKindRXU : dtc::kKindRYU);
+    }
     kind = (kind < 0 || kind == rk) ? rk : dtc::kKindGen;
   }
   return kind;

@@ -98,9 +98,10 @@ static constexpr int kLcMaxLayers = kLcwLayers;
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
-// kKindRXU / kKindRYU: the same families without the unitary factoring (the
-// non-unitary kicks of device-like noise: Kraus x Pauli x RX stays of the
-// RX form), 4 flops per amplitude.
+// kKindRXU / kKindRYU: the same families under device-like noise (one sub-gate
+// per kick): a real Kraus diagonal times the unitary, factored as
+// i^k w diag(rho0, rho1) S, the diagonal deferred to one per-amplitude factor per layer
+// (SiteMat in dtc_kernels.hip), 2 flops per amplitude like RX / RY.
 enum KickKind { kKindRX = 0, kKindRY = 1, kKindGen = 2, kKindRXU = 3, kKindRYU = 4 };
 
 // One layer of single-site kicks on the sites of a pass.
@@ -127,7 +128,8 @@ struct KickDesc {
 // dtc_kernels.hip) — instead of once per tile.  Per (pass, state):
 //   rec[k], rec[12 + k]  pre / post kick of tile bit k
 //       RX/RY family: d[0] = coefficient, i[1] = variant, d[2] = w^2 (the
-//       site's share of the global factor, squared);  general: d[0..7] = 2x2
+//       site's share of the global factor, squared), RXU/RYU: d[3], d[4] = rho0,
+//       rho1 (the deferred Kraus diagonal);  general: d[0..7] = 2x2
 //   rec[24]              d[0], d[1] = global factor (i^k * prod of scales),
 //                        d[2] = 1 / w_post^2 (measurement before the post-kick)
 union KickRec {

@@ -63,30 +63,6 @@ __device__ __forceinline__ void bfly_general(double2& u, double2& v, const doubl
   v = nv;
 }
 
-// RX family, unfactored: [[a, i b], [i c, d]] (a, b, c, d real), 4 flops per amplitude
-__device__ __forceinline__ void bfly_rx(double2& u, double2& v, double a, double b, double c,
-                                        double d) {
-  double2 nu, nv;
-  nu.x = a * u.x - b * v.y;
-  nu.y = a * u.y + b * v.x;
-  nv.x = d * v.x - c * u.y;
-  nv.y = d * v.y + c * u.x;
-  u = nu;
-  v = nv;
-}
-
-// RY family, unfactored: [[a, b], [c, d]] real
-__device__ __forceinline__ void bfly_ry(double2& u, double2& v, double a, double b, double c,
-                                        double d) {
-  double2 nu, nv;
-  nu.x = a * u.x + b * v.x;
-  nu.y = a * u.y + b * v.y;
-  nv.x = c * u.x + d * v.x;
-  nv.y = c * u.y + d * v.y;
-  u = nu;
-  v = nv;
-}
-
 // m <- P m for Pauli code (1 X, 2 Y, 3 Z)
 __device__ __forceinline__ void pauli_left(double2* m, int pauli) {
   if (pauli == 1) {
@@ -194,11 +170,25 @@ __device__ void build_site_kick(const PrepArgs& P, const KickDesc& K, int site, 
 // d = sigma a, c = -sigma b,  M = i^k * w * diag(1, sigma) * R,
 //   form A: R = [[1, beta], [-beta, 1]],  form B: R = [[alpha, 1], [-1, alpha]].
 // General kicks (xy, circular, X-basis) keep the full complex 2x2.
+// Device-like noise (kKindRXU / kKindRYU, one sub-gate per kick): the kick
+// is a real diagonal Kraus factor times a unitary of the family (a Pauli
+// after the Kraus factor moves to its right: X diag(k0, k1) = diag(k1, k0) X;
+// the jump operator is diag(1, 0) X up to its weight), so
+//   M = i^k * w * diag(rho0, rho1) * S,   S as in form A / B below,
+// rho0 = 1 with w, S from the first row (d = rho1 a, c = rho1 b for RX,
+// c = -rho1 b for RY; rho1 = sigma = +-1 when unitary), or rho0 = 0, rho1 = 1
+// with w, S from the second row when the first is zero (a jump followed by an
+// X or Y).  The kernel runs S (var 0 / 2) and defers every site's
+// diag(rho0, rho1): they commute with the other sites' butterflies and with D,
+// so a layer's factors multiply each amplitude once, prod_i rho_{i, x_i} (at
+// the diagonal for the pre-kick, before the store for the post-kick): 2 FMAs
+// per amplitude and site instead of the 4 of the unfactored butterfly.
 struct SiteMat {
   double2 m[4];  // general form
   double coef;   // RX/RY: beta (form A) or alpha (form B)
   double scale;  // RX/RY: w
-  int var;       // RX/RY: (form B ? 2 : 0) | (sigma < 0 ? 1 : 0)
+  double rho0, rho1;  // RXU/RYU: the deferred diag(rho0, rho1)
+  int var;       // RX/RY: (form B ? 2 : 0) | (sigma < 0 ? 1 : 0); RXU/RYU: form B ? 2 : 0
   int k;         // power of i
 };
 
@@ -206,6 +196,8 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
   sm.k = 0;
   sm.coef = 0.0;
   sm.scale = 1.0;
+  sm.rho0 = 1.0;
+  sm.rho1 = 1.0;
   sm.var = 0;
   double a, b, c, d;
   if (kind == kKindRX || kind == kKindRXU) {
@@ -228,9 +220,25 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
     for (int e = 0; e < 4; ++e) sm.m[e] = m[e];
     return;
   }
-  if (kind == kKindRXU || kind == kKindRYU) {  // unfactored: (a, b, c, d) as they are
-    sm.m[0] = make_double2(a, b);
-    sm.m[1] = make_double2(c, d);
+  if (kind == kKindRXU || kind == kKindRYU) {  // factored with a deferred diag(rho0, rho1)
+    const bool rx = kind == kKindRXU;
+    if (a != 0.0 || b != 0.0) {  // from the first row: rho0 = 1
+      const bool form_b = fabs(a) < fabs(b);
+      sm.scale = form_b ? b : a;
+      sm.coef = form_b ? a / b : b / a;
+      sm.var = form_b ? 2 : 0;
+      sm.rho1 = form_b ? (rx ? c / b : -c / b) : d / a;
+    } else if (c != 0.0 || d != 0.0) {  // from the second row: diag(0, 1)
+      // RX: (i c, d) = w (i beta, 1) | w (i, alpha); RY: (c, d) = w (-beta, 1) | w (-1, alpha)
+      const bool form_b = fabs(d) < fabs(c);
+      sm.scale = form_b ? (rx ? c : -c) : d;
+      sm.coef = form_b ? d / sm.scale : (rx ? c / d : -c / d);
+      sm.var = form_b ? 2 : 0;
+      sm.rho0 = 0.0;
+    } else {  // the zero matrix: a zero-weight trajectory
+      sm.scale = 0.0;
+      sm.rho0 = sm.rho1 = 0.0;
+    }
     return;
   }
   // sigma from a d + b c = sigma (a^2 + b^2) (RX) or a d - b c (RY)
@@ -350,8 +358,12 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
           r.d[2 * e + 1] = sm.m[e].y;
         }
       } else if (pk.kind == kKindRXU || pk.kind == kKindRYU) {
-        r.d[0] = sm.m[0].x; r.d[1] = sm.m[0].y; r.d[2] = sm.m[1].x; r.d[3] = sm.m[1].y;
-        for (int e = 4; e < 8; ++e) r.d[e] = 0.0;
+        r.d[0] = sm.coef;
+        r.i[1] = sm.var;
+        r.d[2] = sm.scale * sm.scale;
+        r.d[3] = sm.rho0;
+        r.d[4] = sm.rho1;
+        for (int e = 5; e < 8; ++e) r.d[e] = 0.0;
       } else {
         r.d[0] = sm.coef;
         r.i[1] = sm.var;
@@ -486,13 +498,20 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs&
       for (int r = 0; r < kRegs; ++r)
         if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
     } else if (KIND == kKindRXU || KIND == kKindRYU) {
-      const double a = R.d(k, 0), b = R.d(k, 1), c = R.d(k, 2), d = R.d(k, 3);
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) {
-        if (r & (1 << q)) continue;
-        if (KIND == kKindRXU) bfly_rx(v[r], v[r | (1 << q)], a, b, c, d);
-        else bfly_ry(v[r], v[r | (1 << q)], a, b, c, d);
-      }
+      // S of form A or B only (the sign and the Kraus factor: the deferred
+      // diag(1, rho), rho_apply)
+      constexpr int BK = KIND == kKindRXU ? kKindRX : kKindRY;
+      const double f = R.d(k, 0);
+      const int var = R.i(k, 1);
+      auto run = [&](auto qtag) {
+        constexpr int Q = decltype(qtag)::value;
+        if (var == 0) layer_f<BK, 0, Q>(v, f);
+        else layer_f<BK, 2, Q>(v, f);
+      };
+      if (q == 0) run(std::integral_constant<int, 0>{});
+      else if (q == 1) run(std::integral_constant<int, 1>{});
+      else if (q == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
     } else {
       const double f = R.d(k, 0);
       const int var = R.i(k, 1);
@@ -1134,6 +1153,38 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   };
   const bool x_pre = MC == 3 && (A.meas_parts & kPartXPre);
   const bool x_post = MC == 3 && (A.meas_parts & kPartXPost);
+  // device-like noise: a kick layer's deferred Kraus factors (SiteMat),
+  // prod over the tile bits k of rho_{k, x_k}, in layout LAY (records rec0 ..)
+  constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
+  auto rho_apply = [&](auto lay_tag, int rec0) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const int y = ybase<LAY>(t);
+    double rt = 1.0;
+#pragma unroll
+    for (int k = 0; k < kTileBits; ++k) {
+      if (k >= 4 * LAY && k < 4 * LAY + 4) continue;  // register bits
+      if (!((NIBS >> (k >> 2)) & 1)) continue;        // no kicks: rho = 1
+      rt *= ((y >> k) & 1) ? R.d(rec0 + k, 4) : R.d(rec0 + k, 3);
+    }
+    double f[kRegs];
+    f[0] = rt;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool on = (NIBS >> LAY) & 1;
+      const double r0 = on ? R.d(rec0 + 4 * LAY + q, 3) : 1.0;
+      const double r1 = on ? R.d(rec0 + 4 * LAY + q, 4) : 1.0;
+#pragma unroll
+      for (int r = 0; r < (1 << q); ++r) {
+        f[r | (1 << q)] = f[r] * r1;
+        f[r] *= r0;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      v[r].x *= f[r];
+      v[r].y *= f[r];
+    }
+  };
 
   // ---- pre-kick rounds: 2 -> 0 -> 1 ----
   // (X before a nibble's pre-kick: the state is exact times the factored
@@ -1161,6 +1212,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
   }
   DTC_TS(3);
+  if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0);
   if constexpr (!RP::diag) {
     // no diagonal to carry the kicks' global factor (kick-only pass: no
     // post-kick, so applying it here, before any measurement, is exact)
@@ -1199,6 +1251,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(v, s_tile, s_half, t);
+    if constexpr (kRho) rho_apply(LIO{}, kTileBits);
   } else {
     xch_tile<SPLIT, RP::d_lay, RP::IO>(v, s_tile, s_half, t);
   }
