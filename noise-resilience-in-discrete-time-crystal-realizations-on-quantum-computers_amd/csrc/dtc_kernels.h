@@ -11,6 +11,7 @@ namespace dtc {
 static constexpr int kTileBits = 12;
 static constexpr int kTile = 1 << kTileBits;
 static constexpr int kThreads = 256;
+static constexpr int kWaveSize = 64;
 static constexpr int kRegs = 16;          // amplitudes per thread (4 register bits)
 static constexpr int kChunkBits = 5;      // diagonal factor tables: 5 sites + next bit
 static constexpr int kMaxChunks = 8;      // L_eff <= 40

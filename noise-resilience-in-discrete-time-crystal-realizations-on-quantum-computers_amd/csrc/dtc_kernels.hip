@@ -1319,18 +1319,20 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       if (x_pre || x_post) {
         // (after the stores: meas_finish)
         // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
-        // (0 for sites this pass does not kick)
+        // (0 for sites this pass does not kick); on wave 2 (2L <= 64), beside
+        // wave 0's Z / ZZ combine instead of after it
         const int L = A.L_real;
-        if (t >= 2 * L && t < 4 * L) {
-          const bool pre = t >= 3 * L;
-          const int site = pre ? t - 3 * L : t - 2 * L;
+        const int xo = t - 2 * kWaveSize;
+        if (xo >= 0 && xo < 2 * L) {
+          const bool pre = xo >= L;
+          const int site = pre ? xo - L : xo;
           const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
           double acc = 0.0;
           if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
             const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
             for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
           }
-          A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+          A.partial[(b * n_tiles + tile) * A.n_obs + 2 * L + xo] = acc;
         }
       }
     }

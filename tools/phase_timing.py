@@ -3,7 +3,7 @@
 Build the instrumented library first (SHAPE = 3 records K-D-K passes):
   hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -DDTC_PHASE_TIMING=3 \\
       <pkg>/csrc/dtc_kernels.hip <pkg>/csrc/dtc_engine.cpp -o build/libdtc_timing.so
-then: DTC_LIB=build/libdtc_timing.so python tools/phase_timing.py [batch] [T] [probe|energy]
+then: DTC_LIB=build/libdtc_timing.so python tools/phase_timing.py [batch] [T] [probe|energy|zsite]
 Each workgroup's wave 0 stores s_memtime at: start, setup loads landed, tables
 ready (barrier), pre-kick rounds done, diagonal done, post-kick rounds done,
 stores issued.  The buffer keeps the last recorded launch."""
@@ -32,6 +32,8 @@ os.environ["DTC_DBG_PTR"] = str(buf.data_ptr())
 eng = pkg.DtcEngine(0)
 if len(sys.argv) > 3 and sys.argv[3] == "energy":
     eng.energy(spec, B, batch=B)
+elif len(sys.argv) > 3 and sys.argv[3] == "zsite":
+    eng.autocorr(spec, B, batch=B, want_zsite=True, want_echo=False)
 else:
     eng.autocorr(spec, B, batch=B)
 torch.cuda.synchronize()
