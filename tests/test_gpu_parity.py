@@ -204,6 +204,11 @@ def test_noise_sampler_unbiased_high_resolution(pkg, engine):
     (16, 6, 0.1, "vacuum", "x", 0, 5),
     (18, 6, 0.1, "vacuum", "x", 1, 13),
     (22, 8, 0.05, "vacuum", "y", 0, None),
+    # the 10-site window at its edges (j - 4 = 2, j + 3 = L - 1), next to a
+    # 9-site second group (L = 21: 128-B columns), with t_offset and RY kicks
+    (16, 7, 0.1, "neel", "x", 0, 6),
+    (16, 7, 0.1, "vacuum", "y", 1, 12),
+    (21, 7, 0.1, "vacuum", "y", 0, None),
 ])
 def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe):
     """Echo chains ending in the light-cone pass (the chain's last passes merged

@@ -36,21 +36,34 @@ one = unit * reps / (time.time() - t0)
 print(f"one engine, {N} per call: {one:.0f} periods*traj/s", flush=True)
 
 
-def run(eng, off):
+durs = {0: [], 1: []}
+
+
+def run(k, eng, off, delay):
+    time.sleep(delay)
     for r in range(reps):
+        t = time.time()
         eng.autocorr(spec, N // 2, batch=N // 2, traj_offset=off + r * N)
+        durs[k].append(time.time() - t)
 
 
+half_step = N * 464 / one / 2  # seconds: half of one N-trajectory call
 t0 = time.time()
-th = [threading.Thread(target=run, args=(e, o)) for e, o in ((e1, 0), (e2, N // 2))]
+th = [threading.Thread(target=run, args=(k, e, o, d))
+      for k, e, o, d in ((0, e1, 0, 0.0), (1, e2, N // 2, half_step / 2))]
 for t in th:
     t.start()
 for t in th:
     t.join()
 torch.cuda.synchronize()
 two = unit * reps / (time.time() - t0)
-print(f"two engines concurrently, {N // 2} each: {two:.0f} periods*traj/s ({two / one:.3f}x)",
-      flush=True)
+print(f"two engines concurrently, {N // 2} each, second started {half_step / 2:.2f} s late: "
+      f"{two:.0f} periods*traj/s ({two / one:.3f}x)", flush=True)
+import numpy as np  # noqa: E402
+mid = [d for k in (0, 1) for d in durs[k][1:-1]]
+print(f"  call durations (s): {[round(d, 3) for d in durs[0]]} / {[round(d, 3) for d in durs[1]]}; "
+      f"middle calls median {np.median(mid):.3f} s = {(N // 2) * 464 * 2 / np.median(mid):.0f} "
+      f"periods*traj/s for the pair", flush=True)
 t0 = time.time()
 for r in range(reps):
     e1.autocorr(spec, N // 2, batch=N // 2, traj_offset=r * N)
