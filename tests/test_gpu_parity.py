@@ -194,23 +194,26 @@ def test_noise_sampler_unbiased_high_resolution(pkg, engine):
     assert se / (1 - p) ** 8 < 5e-4
 
 
-@pytest.mark.parametrize("L,T,p,state,pol,toff,probe", [
-    (20, 7, 0.1, "vacuum", "x", 0, None),
-    (20, 6, 0.05, "neel", "xy", 1, None),
-    (21, 6, 0.1, "vacuum", "circular_left", 0, None),
-    (21, 5, 0.0, "vacuum", "y", 0, None),
-    (12, 6, 0.1, "vacuum", "x", 0, None),
-    (14, 7, 0.1, "neel", "y", 0, None),
-    (16, 6, 0.1, "vacuum", "x", 0, 5),
-    (18, 6, 0.1, "vacuum", "x", 1, 13),
-    (22, 8, 0.05, "vacuum", "y", 0, None),
-    # the 10-site window at its edges (j - 4 = 2, j + 3 = L - 1), next to a
-    # 9-site second group (L = 21: 128-B columns), with t_offset and RY kicks
-    (16, 7, 0.1, "neel", "x", 0, 6),
-    (16, 7, 0.1, "vacuum", "y", 1, 12),
-    (21, 7, 0.1, "vacuum", "y", 0, None),
+@pytest.mark.parametrize("L,T,p,state,pol,toff,probe,wide", [
+    # wide: the 10-site window merges five passes somewhere (True), or the
+    # layers do not fit it and every chain keeps the 8-site form (False)
+    (20, 7, 0.1, "vacuum", "x", 0, None, True),
+    (20, 6, 0.05, "neel", "xy", 1, None, False),        # general kicks: no light cone
+    (21, 6, 0.1, "vacuum", "circular_left", 0, None, False),
+    (21, 5, 0.0, "vacuum", "y", 0, None, None),
+    (12, 6, 0.1, "vacuum", "x", 0, None, None),
+    (14, 7, 0.1, "neel", "y", 0, None, True),
+    (16, 6, 0.1, "vacuum", "x", 0, 5, False),            # j - 4 < 2
+    (18, 6, 0.1, "vacuum", "x", 1, 13, True),
+    (22, 8, 0.05, "vacuum", "y", 0, None, False),        # three site groups
+    # edges: j - 4 = 2 with the first layer's group spanning sites 1 .. 11 (11
+    # sites: too wide), j + 3 = L - 1, and a 9-site second group (L = 21:
+    # 128-B columns), with t_offset and RY kicks
+    (16, 7, 0.1, "neel", "x", 0, 6, False),
+    (16, 7, 0.1, "vacuum", "y", 1, 12, True),
+    (21, 7, 0.1, "vacuum", "y", 0, None, True),
 ])
-def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe):
+def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe, wide):
     """Echo chains ending in the light-cone pass (the chain's last passes merged
     into one measure-only pass, each kick layer cut to the light cone of Z_j):
     five passes over a 10-site window (dtc_lcw_final) where it fits, else four
@@ -245,10 +248,8 @@ def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe)
     assert n_wide <= n_narrow <= n_full
     if pol in ("x", "y"):  # factored kicks (general 2x2 kicks keep the full passes)
         assert n_narrow < n_full
-        j = spec.probe_site
-        # two site groups (L <= 21: five passes = six layers), the window inside
-        if j - 4 >= 2 and j + 3 <= L - 1 and T >= 6 and L <= 21:
-            assert n_wide < n_narrow  # the 10-site window merged a fifth pass somewhere
+    if wide is not None:
+        assert (n_wide < n_narrow) == wide, (n_wide, n_narrow)
 
 
 def test_independent_t_matches_oracle(pkg, engine):
