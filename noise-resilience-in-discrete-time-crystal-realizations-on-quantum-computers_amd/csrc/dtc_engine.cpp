@@ -77,6 +77,7 @@ struct dtc_ctx {
   hipStream_t stream = nullptr;
   DevBuf F, E, partial, vals_f, vals_e, diag, kick, basis, sitemap;
   DevBuf lc_diag;  // cone diagonals of the light-cone pass, [n_inst][kLcTab]
+  DevBuf red_scratch;  // split sums of the two-stage tile reduction (large states)
   DevBuf recs, recs1, pk;               // kick records (batch schedule / single pass), pass list
   DevBuf dev_thr, dev_jump, dev_kraus;  // device-like noise tables (dtc_autocorr_device)
   std::vector<dtc::PassKick> pk_host;   // staged pass list (alive until the stream syncs)
@@ -428,8 +429,19 @@ int launch_reduce_prof(dtc_ctx* ctx, int n_tiles, int n_obs, int batch, double* 
     e1 = get_event(ctx);
     DTC_HIP(hipEventRecord(e0, ctx->stream));
   }
+  double* scratch = nullptr;
+  if (dtc::reduce_splits(n_tiles) > 1) {
+    // split sums of a large state's tiles ([batch][splits][n_out])
+    const int no = n_out < 0 ? n_obs - o_first : n_out;
+    const size_t need = (size_t)batch * dtc::reduce_splits(n_tiles) * no * sizeof(double);
+    if (ctx->red_scratch.n < need) {
+      DTC_HIP(hipStreamSynchronize(ctx->stream));  // the previous scratch may be in use
+      DTC_TRY(ensure(ctx->red_scratch, need));
+    }
+    scratch = (double*)ctx->red_scratch.p;
+  }
   DTC_HIP(dtc::launch_reduce((const double*)ctx->partial.p, n_tiles, n_obs, batch, out,
-                             out_stride, ctx->stream, o_first, n_out, accumulate));
+                             out_stride, ctx->stream, o_first, n_out, accumulate, scratch));
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     ctx->pending.push_back(
@@ -1122,6 +1134,7 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->vals_e);
   release(ctx->diag);
   release(ctx->lc_diag);
+  release(ctx->red_scratch);
   release(ctx->kick);
   release(ctx->basis);
   release(ctx->sitemap);

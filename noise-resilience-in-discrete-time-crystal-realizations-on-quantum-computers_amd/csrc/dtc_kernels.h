@@ -258,10 +258,15 @@ hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);
 
 // out[b * out_stride + o] = sum over tiles of partial[b][tile][o_first + o],
-// o < n_out (fixed order); accumulate: += instead of =
+// o < n_out (fixed order); accumulate: += instead of =.  Large states
+// (reduce_splits(n_tiles) > 1) sum in two stages, split sums into `scratch`
+// ([batch][splits][n_out] doubles): the order depends on n_tiles only, so a
+// state's result does not depend on the batch it ran in.
+__host__ __device__ constexpr int reduce_splits(int n_tiles) { return n_tiles >= 1024 ? n_tiles / 512 : 1; }
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
                          double* out, int64_t out_stride, hipStream_t stream,
-                         int o_first = 0, int n_out = -1, int accumulate = 0);
+                         int o_first = 0, int n_out = -1, int accumulate = 0,
+                         double* scratch = nullptr);
 
 // amplitude idx[b] of state b = 1 (after the caller zeroed the batch), in the
 // batch layout of octet_bits (state_base / octet_spread)

@@ -1971,20 +1971,22 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
                                                      int n_tiles, int n_obs, int o_first,
                                                      int n_out, int cols, int accumulate,
                                                      double* __restrict__ out,
-                                                     int64_t out_stride) {
+                                                     int64_t out_stride, int splits) {
   __shared__ double s_acc[256];
-  const int b = blockIdx.y, t = threadIdx.x;
+  const int b = blockIdx.y, t = threadIdx.x, z = blockIdx.z;
   const int o = blockIdx.x * cols + t % cols, grp = t / cols, ngrp = 256 / cols;
+  // split z of `splits` sums tiles [k0, k1) (stage 1 of a two-stage sum)
+  const int per = n_tiles / splits, k0 = z * per, k1 = k0 + per;
   double acc = 0.0;
   if (o < n_out) {
     const double* p = partial + (int64_t)b * n_tiles * n_obs + o_first + o;
     double a2[4] = {0.0, 0.0, 0.0, 0.0};
-    int k = grp;
-    for (; k + 3 * ngrp < n_tiles; k += 4 * ngrp) {
+    int k = k0 + grp;
+    for (; k + 3 * ngrp < k1; k += 4 * ngrp) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) a2[u] += p[(int64_t)(k + u * ngrp) * n_obs];
     }
-    for (; k < n_tiles; k += ngrp) a2[0] += p[(int64_t)k * n_obs];
+    for (; k < k1; k += ngrp) a2[0] += p[(int64_t)k * n_obs];
     acc = (a2[0] + a2[1]) + (a2[2] + a2[3]);
   }
   s_acc[t] = acc;
@@ -1992,19 +1994,38 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   if (grp == 0 && o < n_out) {
     double sum = s_acc[t];
     for (int g = 1; g < ngrp; ++g) sum += s_acc[g * cols + t];
-    double* dst = out + (int64_t)b * out_stride + o;
-    *dst = accumulate ? *dst + sum : sum;
+    if (splits > 1) {
+      out[((int64_t)b * splits + z) * n_out + o] = sum;  // scratch: [batch][splits][n_out]
+    } else {
+      double* dst = out + (int64_t)b * out_stride + o;
+      *dst = accumulate ? *dst + sum : sum;
+    }
   }
 }
 
 hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batch,
                          double* out, int64_t out_stride, hipStream_t stream, int o_first,
-                         int n_out, int accumulate) {
+                         int n_out, int accumulate, double* scratch) {
   if (n_out < 0) n_out = n_obs - o_first;
   if (o_first < 0 || n_out < 1 || o_first + n_out > n_obs) return hipErrorInvalidValue;
-  const int cols = n_out <= 16 ? 16 : (n_out <= 32 ? 32 : (n_out <= 64 ? 64 : (n_out <= 128 ? 128 : 256)));
-  hipLaunchKernelGGL(reduce_kernel, dim3((n_out + cols - 1) / cols, batch), dim3(256), 0, stream,
-                     partial, n_tiles, n_obs, o_first, n_out, cols, accumulate, out, out_stride);
+  auto cols_of = [](int n) {
+    return n <= 16 ? 16 : (n <= 32 ? 32 : (n <= 64 ? 64 : (n <= 128 ? 128 : 256)));
+  };
+  const int cols = cols_of(n_out);
+  const int splits = reduce_splits(n_tiles);
+  if (splits > 1) {
+    // two stages: every (state, split) a workgroup, then the splits in order
+    if (!scratch || n_tiles % splits) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(reduce_kernel, dim3((n_out + cols - 1) / cols, batch, splits), dim3(256), 0,
+                       stream, partial, n_tiles, n_obs, o_first, n_out, cols, 0, scratch,
+                       (int64_t)0, splits);
+    hipLaunchKernelGGL(reduce_kernel, dim3((n_out + cols - 1) / cols, batch, 1), dim3(256), 0,
+                       stream, (const double*)scratch, splits, n_out, 0, n_out, cols, accumulate,
+                       out, out_stride, 1);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(reduce_kernel, dim3((n_out + cols - 1) / cols, batch, 1), dim3(256), 0, stream,
+                     partial, n_tiles, n_obs, o_first, n_out, cols, accumulate, out, out_stride, 1);
   return hipGetLastError();
 }
 
