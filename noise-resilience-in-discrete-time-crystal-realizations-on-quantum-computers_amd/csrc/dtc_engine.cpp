@@ -59,6 +59,14 @@ struct DevBuf {
   size_t n = 0;
 };
 
+// Pinned host staging for the per-trajectory results copied back after a
+// batch (direct DMA, no zero-filled pageable vector per call).
+struct HostBuf {
+  double* p = nullptr;
+  size_t n = 0;  // doubles
+};
+
+
 struct Group {
   int c, s;  // tile = bits [0, c) + [s, s + 12 - c)
   int act;   // active tile-bit mask
@@ -98,6 +106,7 @@ struct dtc_ctx {
   int lc_split = 1;          // DTC_LC_SPLIT
   int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
   bool lc_wide = true;       // DTC_NO_LCW unset: five-pass (10-site) light-cone ends
+  HostBuf host_f, host_e;    // pinned result staging (autocorr / energy)
   uint64_t tables_key = 0;   // upload_tables: the problem whose tables are in place
   bool tables_valid = false;
   // DTC_KDK_SPLIT: which K-D-K passes run three workgroups per CU (dtc_kernels.h
@@ -137,6 +146,17 @@ int ensure(DevBuf& b, size_t bytes) {
   }
   DTC_HIP(hipMalloc(&b.p, bytes));
   b.n = bytes;
+  return DTC_OK;
+}
+
+int ensure_host(HostBuf& b, size_t n) {
+  if (n == 0) n = 1;
+  if (b.n >= n) return DTC_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  DTC_HIP(hipHostMalloc((void**)&b.p, n * sizeof(double), hipHostMallocDefault));
+  b.n = n;
   return DTC_OK;
 }
 
@@ -1159,6 +1179,8 @@ int dtc_close(dtc_ctx* ctx) {
   release(ctx->diag);
   release(ctx->lc_diag);
   release(ctx->red_scratch);
+  if (ctx->host_f.p) (void)hipHostFree(ctx->host_f.p);
+  if (ctx->host_e.p) (void)hipHostFree(ctx->host_e.p);
   release(ctx->kick);
   release(ctx->basis);
   release(ctx->sitemap);
@@ -1407,7 +1429,10 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   if (want_e) DTC_TRY(ensure(ctx->vals_e, (size_t)B * T * 2 * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
 
-  std::vector<double> hv_f((size_t)B * T * n_obs_f), hv_e(want_e ? (size_t)B * T * 2 : 0);
+  DTC_TRY(ensure_host(ctx->host_f, (size_t)B * T * n_obs_f));
+  if (want_e) DTC_TRY(ensure_host(ctx->host_e, (size_t)B * T * 2));
+  double* const hv_f = ctx->host_f.p;
+  double* const hv_e = ctx->host_e.p;
   std::vector<int64_t> masks(B);
 
   for (int64_t bs = 0; bs < S; bs += B) {
@@ -1497,10 +1522,10 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     }
     if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
-    DTC_HIP(hipMemcpyAsync(hv_f.data(), ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
+    DTC_HIP(hipMemcpyAsync(hv_f, ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
     if (want_e)
-      DTC_HIP(hipMemcpyAsync(hv_e.data(), ctx->vals_e.p, (size_t)nb * T * 2 * sizeof(double),
+      DTC_HIP(hipMemcpyAsync(hv_e, ctx->vals_e.p, (size_t)nb * T * 2 * sizeof(double),
                              hipMemcpyDeviceToHost, ctx->stream));
     DTC_HIP(hipStreamSynchronize(ctx->stream));
     DTC_TRY(settle_pending(ctx));
@@ -1512,7 +1537,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       const double zinit = ((m >> j) & 1ull) ? -1.0 : 1.0;
       for (int t = std::max(0, pr->t_first); t < T; ++t) {
         const bool at_init = (t + pr->t_offset == 0);
-        const double* vf = hv_f.data() + ((size_t)b * T + t) * n_obs_f;
+        const double* vf = hv_f + ((size_t)b * T + t) * n_obs_f;
         const double zj_f = at_init ? zinit : (want_z ? vf[1 + j] : vf[1]);
         if (pr->want_fwd) fwd[(size_t)g * T + t] = ro_a * (fac * zinit * zj_f) + ro_b;
         if (want_z) {
@@ -1758,7 +1783,8 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_v * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
-  std::vector<double> hv_f((size_t)B * T * n_v);
+  DTC_TRY(ensure_host(ctx->host_f, (size_t)B * T * n_v));
+  double* const hv_f = ctx->host_f.p;
   std::vector<int64_t> masks(B);
 
   // The schedule: the forward chain one kick layer past the last period
@@ -1892,7 +1918,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                                    vals + (size_t)e.t_mid * n_v + 2 * L, vs, 1, L, 1));
       }
     }
-    DTC_HIP(hipMemcpyAsync(hv_f.data(), vals, (size_t)nb * T * n_v * sizeof(double),
+    DTC_HIP(hipMemcpyAsync(hv_f, vals, (size_t)nb * T * n_v * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
     DTC_HIP(hipStreamSynchronize(ctx->stream));
     DTC_TRY(settle_pending(ctx));
@@ -1901,7 +1927,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
       const uint64_t m = (uint64_t)masks[b];
       for (int t = 0; t < T; ++t) {
         const bool at_init = (t + pr->t_offset == 0);
-        const double* vf = hv_f.data() + ((size_t)b * T + t) * n_v;
+        const double* vf = hv_f + ((size_t)b * T + t) * n_v;
         const double* vx = vf + 2 * L - 1;  // X_i at vx[1 + i]
         double* zo = z + ((size_t)g * T + t) * L;
         double* xo = x + ((size_t)g * T + t) * L;

@@ -1,0 +1,9 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_energy.py -k "light_cone or energy" > gpurun_out/r3zh_tests.txt 2>&1 || exit 1
+DTC_LIB=$GRAFT_REPO_ROOT/devlib/libdtc_lcw_pred.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "light_cone" >> gpurun_out/r3zh_tests.txt 2>&1 || exit 1
+for i in 1 2; do
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r3zh_c2_base_$i.json 2>/dev/null && \
+DTC_LIB=$GRAFT_REPO_ROOT/devlib/libdtc_lcw_pred.so timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r3zh_c2_pred_$i.json 2>/dev/null && \
+timeout -k 10 200 python bench.py --config energy --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r3zh_energy_$i.json 2>/dev/null || exit 1
+done
