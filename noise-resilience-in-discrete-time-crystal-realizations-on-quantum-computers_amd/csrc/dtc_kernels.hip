@@ -1042,7 +1042,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   };
   // Per-site / energy Z, ZZ partials of the tile from the wave sums in s_red
   // (layout lay of the measurement): one observable per thread t < n_mid.
-  auto site_combine = [&](int lay, double inv_w2) {
+  auto site_combine = [&](int lay, double inv_w2, int t) {
     const bool energy = MC >= 2 && A.meas == kMeasEnergy;
     const int n_mid = energy ? 2 * A.L_real : 1 + A.L_real;
     if (t >= n_mid) return;
@@ -1313,28 +1313,26 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
         }
       }
     }
+    // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
+    // (0 for sites this pass does not kick), observable 2L + xo
+    auto x_combine = [&](int xo) {
+      const int L = A.L_real;
+      if (xo < 0 || xo >= 2 * L) return;
+      const bool pre = xo >= L;
+      const int site = pre ? xo - L : xo;
+      const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
+      double acc = 0.0;
+      if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
+        const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
+        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
+      }
+      A.partial[(b * n_tiles + tile) * A.n_obs + 2 * L + xo] = acc;
+    };
     if (zc_lay >= 0 || x_pre || x_post) {
       __syncthreads();
-      if (zc_lay >= 0) site_combine(zc_lay, zc_inv);
-      if (x_pre || x_post) {
-        // (after the stores: meas_finish)
-        // obs [2L, 3L): X before the post-kick, [3L, 4L): X before the pre-kick
-        // (0 for sites this pass does not kick); on wave 2 (2L <= 64), beside
-        // wave 0's Z / ZZ combine instead of after it
-        const int L = A.L_real;
-        const int xo = t - 2 * kWaveSize;
-        if (xo >= 0 && xo < 2 * L) {
-          const bool pre = xo >= L;
-          const int site = pre ? xo - L : xo;
-          const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
-          double acc = 0.0;
-          if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
-            const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
-            for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
-          }
-          A.partial[(b * n_tiles + tile) * A.n_obs + 2 * L + xo] = acc;
-        }
-      }
+      if (zc_lay >= 0) site_combine(zc_lay, zc_inv, t);
+      // X on wave 2 (2L <= 64), beside wave 0's Z / ZZ combine
+      if (x_pre || x_post) x_combine(t - 2 * kWaveSize);
     }
   }
 #ifdef DTC_PHASE_TIMING
