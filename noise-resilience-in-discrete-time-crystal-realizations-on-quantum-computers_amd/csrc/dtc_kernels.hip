@@ -1624,7 +1624,27 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lc_final_split(PassArgs A) {
 // — six re-layouts through the 32 KiB half-tile buffer for five passes (the
 // 8-site pass: five for four), three workgroups per CU.  D5 is two lookups
 // in the split radius-5 tables.  Global indices fit 32 bits (L_eff <= 32).
-template <int KIND>
+// MASK: the layers' kick mask when known at compile time (0: read A.lc_mask).
+// The chains of the C2 sweep (two site groups split at j+2, the first merged
+// pass on j's group) all have kLcwMaskJ2 (lc_merge_wide): its instantiation
+// runs exactly the 32 kicked sites with no per-site branches, so the compiler
+// keeps the butterflies' results in renamed registers instead of copying them
+// back for the branch merges.
+static constexpr uint64_t kLcwMaskJ2 =
+    // l = 0: tile bits 2, 4..7, 10, 11 (sites j-5, j-2..j+1, j-4, j-3)
+    (0x33Dull) |
+    // l = 1: tile bits 3..11 (j+4, j-2..j+3, j-4, j-3)
+    (0x3FEull << 10) |
+    // l = 2: tile bits 4..9, 11 (j-2..j+3, j-3)
+    (0x2FCull << 20) |
+    // l = 3: tile bits 4..8 (j-2..j+2)
+    (0x07Cull << 30) |
+    // l = 4: tile bits 5..7 (j-1..j+1)
+    (0x038ull << 40) |
+    // l = 5: tile bit 6 (j)
+    (0x010ull << 50);
+
+template <int KIND, uint64_t MASK = 0>
 __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
   __shared__ double s_half[kTile];
@@ -1720,13 +1740,23 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
   auto kick = [&](auto n_tag, auto l_tag) {
     constexpr int N = decltype(n_tag)::value;
     constexpr int l = decltype(l_tag)::value;
-    const uint32_t m = (uint32_t)(A.lc_mask >> (10 * l));
-    if constexpr (4 * N + 0 >= 2)
-      if ((m >> (4 * N + 0 - 2)) & 1u) layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
-    if constexpr (4 * N + 1 >= 2)
-      if ((m >> (4 * N + 1 - 2)) & 1u) layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
-    if ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
-    if ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
+    if constexpr (MASK != 0) {
+      constexpr uint32_t m = (uint32_t)(MASK >> (10 * l));
+      if constexpr (4 * N + 0 >= 2 && ((m >> (4 * N + 0 - 2)) & 1u))
+        layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
+      if constexpr (4 * N + 1 >= 2 && ((m >> (4 * N + 1 - 2)) & 1u))
+        layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
+      if constexpr ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
+      if constexpr ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
+    } else {
+      const uint32_t m = (uint32_t)(A.lc_mask >> (10 * l));
+      if constexpr (4 * N + 0 >= 2)
+        if ((m >> (4 * N + 0 - 2)) & 1u) layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
+      if constexpr (4 * N + 1 >= 2)
+        if ((m >> (4 * N + 1 - 2)) & 1u) layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
+      if ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
+      if ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
+    }
   };
   // one cone-table factor in layout LAY: tab[((x ^ m) >> lo) & msk] per amplitude
   auto diag_tab = [&](auto lay_tag, uint32_t xm, int lo, int hi, const double2* tab) {
@@ -1911,8 +1941,13 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
       if (a.lc_gb[k] < 0 || a.lc_gb[k] >= a.L_eff || ((seen >> a.lc_gb[k]) & 1)) return hipErrorInvalidValue;
       seen |= 1ull << a.lc_gb[k];
     }
-    hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX> : dtc_lcw_final<kKindRY>), grid,
-                       dim3(kThreads), 0, stream, a);
+    if (a.lc_mask == kLcwMaskJ2)
+      hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX, kLcwMaskJ2>
+                                          : dtc_lcw_final<kKindRY, kLcwMaskJ2>),
+                         grid, dim3(kThreads), 0, stream, a);
+    else
+      hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX> : dtc_lcw_final<kKindRY>), grid,
+                         dim3(kThreads), 0, stream, a);
     return hipGetLastError();
   }
   if (shape == kShapeLC) {
