@@ -844,8 +844,9 @@ void build_cone_tables(int L, int j, int n_inst, const double* h, const double* 
       double* o = out.data() + ((size_t)in * dtc::kLcTab + dtc::lc_tab_off(r)) * 2;
       for (int v = 0; v < (1 << (hi - lo + 1)); ++v) {
         const double ang = diag_angle(L, hh, pp, std::max(0, j - r + 1), j + r, j - r, j + r, lo, v);
-        o[2 * v] = std::cos(-0.5 * ang);
-        o[2 * v + 1] = std::sin(-0.5 * ang);
+        const int e = r == 4 ? dtc::lc_pos4(v) : v;  // the radius-4 table's storage swizzle
+        o[2 * e] = std::cos(-0.5 * ang);
+        o[2 * e + 1] = std::sin(-0.5 * ang);
       }
     }
     for (int part = 0; part < 2; ++part) {
@@ -856,8 +857,9 @@ void build_cone_tables(int L, int j, int n_inst, const double* h, const double* 
         const double ang = part == 0
                                ? diag_angle(L, hh, pp, std::max(0, j - 4), j + 1, j - 5, j, lo, v)
                                : diag_angle(L, hh, pp, j + 1, j + 5, j, j + 5, lo, v);
-        o[2 * v] = std::cos(-0.5 * ang);
-        o[2 * v + 1] = std::sin(-0.5 * ang);
+        const int e = part == 0 ? dtc::lc_pos5a(v) : v;  // storage swizzle of the j-5 .. j table
+        o[2 * e] = std::cos(-0.5 * ang);
+        o[2 * e + 1] = std::sin(-0.5 * ang);
       }
     }
   }

@@ -80,6 +80,13 @@ __host__ __device__ constexpr int lc_tab_off(int r) { return ((1 << (2 * r + 1))
 // bonds (j-5, j-4) .. (j-1, j)) and bits j .. j+5 (fields j+1 .. j+4, bonds
 // (j, j+1) .. (j+4, j+5)), clipped to [0, L): two lookups instead of a
 // 2048-entry table (which would leave LDS for two workgroups per CU only).
+// Storage swizzles of the tables whose lookups in the 10-site pass index by
+// lane bits 256 B apart (one LDS bank group): entry i of the radius-4 table
+// sits at lc_pos4(i), of the j-5 .. j table at lc_pos5a(i) -- XOR folds of the
+// lane-varying index bits into the low bits, linear, so a lookup base ^ offset
+// becomes pos(base) ^ pos(offset) at no cost per amplitude.
+__host__ __device__ constexpr int lc_pos4(int i) { return i ^ ((i >> 8) & 1); }
+__host__ __device__ constexpr int lc_pos5a(int i) { return i ^ ((i >> 4) & 3); }
 static constexpr int kLcTab5a = kLcTab4;
 static constexpr int kLcTab5b = kLcTab4 + 64;
 static constexpr int kLcTab = kLcTab4 + 128;  // per-instance stride of PassArgs::lc_diag

@@ -1508,7 +1508,8 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
       const int off = (g0 >= lo ? (r << (g0 - lo)) : (r >> (lo - g0))) & msk;
-      v[r] = cmul(v[r], tab[base ^ off]);
+      const int i = base ^ off;
+      v[r] = cmul(v[r], tab[rad == 4 ? lc_pos4(i) : i]);  // (the radius-4 table's storage)
     }
   };
   using L1 = std::integral_constant<int, 1>;
@@ -1759,12 +1760,16 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
     }
   };
   // one cone-table factor in layout LAY: tab[((x ^ m) >> lo) & msk] per amplitude
-  auto diag_tab = [&](auto lay_tag, uint32_t xm, int lo, int hi, const double2* tab) {
+  // sw: the table's storage swizzle (0 none, 4 lc_pos4, 5 lc_pos5a), applied to
+  // the thread's base and the register offsets once (linear)
+  auto diag_tab = [&](auto lay_tag, uint32_t xm, int lo, int hi, const double2* tab, auto sw_tag) {
     constexpr int LAY = decltype(lay_tag)::value;
+    constexpr int SW = decltype(sw_tag)::value;
+    auto pos = [](int i) { return SW == 4 ? lc_pos4(i) : (SW == 5 ? lc_pos5a(i) : i); };
     const uint32_t msk = (1u << (hi - lo + 1)) - 1u;
-    const int base = (int)((xm >> lo) & msk);
-    const int o0 = (int)((gbit[4 * LAY] >> lo) & msk), o1 = (int)((gbit[4 * LAY + 1] >> lo) & msk);
-    const int o2 = (int)((gbit[4 * LAY + 2] >> lo) & msk), o3 = (int)((gbit[4 * LAY + 3] >> lo) & msk);
+    const int base = pos((int)((xm >> lo) & msk));
+    const int o0 = pos((int)((gbit[4 * LAY] >> lo) & msk)), o1 = pos((int)((gbit[4 * LAY + 1] >> lo) & msk));
+    const int o2 = pos((int)((gbit[4 * LAY + 2] >> lo) & msk)), o3 = pos((int)((gbit[4 * LAY + 3] >> lo) & msk));
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
       const int off = ((r & 1) ? o0 : 0) ^ ((r & 2) ? o1 : 0) ^ ((r & 4) ? o2 : 0) ^ ((r & 8) ? o3 : 0);
@@ -1776,11 +1781,15 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
     constexpr int l = decltype(l_tag)::value;
     constexpr int rad = kLcwLayers - 1 - l;
     const uint32_t xm = (tbase | lane_part(lay_tag)) ^ (uint32_t)R.bits(kLcwMask + l);
+    using S0 = std::integral_constant<int, 0>;
     if constexpr (rad == 5) {
-      diag_tab(lay_tag, xm, max(0, jp - 5), jp, s_cone + kLcTab5a);
-      diag_tab(lay_tag, xm, jp, min(Lr - 1, jp + 5), s_cone + kLcTab5b);
+      diag_tab(lay_tag, xm, max(0, jp - 5), jp, s_cone + kLcTab5a, std::integral_constant<int, 5>{});
+      diag_tab(lay_tag, xm, jp, min(Lr - 1, jp + 5), s_cone + kLcTab5b, S0{});
+    } else if constexpr (rad == 4) {
+      diag_tab(lay_tag, xm, max(0, jp - 4), min(Lr - 1, jp + 4), s_cone + lc_tab_off(4),
+               std::integral_constant<int, 4>{});
     } else {
-      diag_tab(lay_tag, xm, max(0, jp - rad), min(Lr - 1, jp + rad), s_cone + lc_tab_off(rad));
+      diag_tab(lay_tag, xm, max(0, jp - rad), min(Lr - 1, jp + rad), s_cone + lc_tab_off(rad), S0{});
     }
   };
   using C0 = std::integral_constant<int, 0>;
