@@ -6,6 +6,12 @@ PKG     := noise-resilience-in-discrete-time-crystal-realizations-on-quantum-com
 ARCH    ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -Wall -Wno-unused-result
 HIPCFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+# `make DEV=1 ...`: development A/B build whose dtc_open honours the layout /
+# geometry override variables (DTC_OCTET_BITS, DTC_LC_SPLIT, DTC_LC_TPB,
+# DTC_KDK_SPLIT, DTC_BATCH_BYTES, DTC_NO_BASIS_SYNTH); never the product
+ifeq ($(DEV),1)
+HIPCFLAGS += -DDTC_DEV_KNOBS
+endif
 # CPU oracle (test infrastructure): portable build, plus an x86-64-v3 build
 # that is loaded only on hosts with those features.
 ORACLE_MARCH ?= x86-64-v2

@@ -278,7 +278,7 @@ def spawn_selftest(args) -> int:
     if os.environ.get("BENCH_SELFTEST_HANG") == "1":
         time.sleep(3600)  # test hook: a nested rank that never finishes
     if rank == 0:
-        B = args.strong_total // world if args.strong_total else args.batch
+        B = args.strong_total // world if args.strong_total else (args.batch or 256)
         d = {"metric": "spawn-selftest", "value": float(t[0]), "n_gpus": world,
              "rank_sum": float(t[1]), "scaling": "strong" if args.strong_total else "weak",
              "trajectories_per_step_per_gpu": B}
@@ -341,8 +341,9 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256,
-                    help="trajectories per step per GPU when --strong-total is 0 (weak scaling)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="trajectories per step per GPU when --strong-total is 0 (weak scaling); "
+                         "0 = the config's default (c2: 256, c3 and energy: 1024)")
     ap.add_argument("--strong-total", type=int, default=1024,
                     help="c2/c3: trajectories per step over ALL ranks, split evenly (strong "
                          "scaling, the north_star's 1 -> 8 GPU target; default 1024); 0 = weak "
@@ -369,7 +370,8 @@ def main(argv=None):
                          "device-like noise (stand-in calibration, data/"
                          "device_standin_L20.json), 1024 trajectories per step; c4: L=28 "
                          "noiseless disorder sweep, instances sharded over ranks; c5: one "
-                         "L=34 state sharded over the ranks (1 GPU: --L 31, 8 virtual ranks); "
+                         "L=34 state sharded over the ranks (1 GPU: L=34 as 8 virtual ranks "
+                         "with the in-place exchange; --L 31 or less: the two-buffer form); "
                          "energy: the energy observable path (§8(f)1); ctrl: the real-time "
                          "adaptive-g controller loop (§8(f)2)")
     ap.add_argument("--ctrl-tf", type=int, default=20, help="ctrl: time points of the loop")
@@ -423,8 +425,8 @@ def main(argv=None):
         cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data",
                                                            "device_standin_L20.json"))
         spec.device = cal.device_noise(args.L)
-        if args.batch == 256:
-            args.batch = 1024
+    if not args.batch:
+        args.batch = 1024 if c3 else 256
     eng = pkg.DtcEngine(dev)
     B = args.batch
     if args.strong_total:
@@ -974,7 +976,7 @@ def main_energy(args):
     # 1024 trajectories per step unless --batch says otherwise: the per-call host
     # work (result copies and their unpacking) then stays near 2 % of a step
     # (r3zn: 145.2k at 1024 vs 138.4k at 256 on one box)
-    if args.batch == 256:
+    if not args.batch:
         args.batch = 1024
     L, T, B = args.L, args.tf, args.batch
     hs, phis = load_disorder_row(L)

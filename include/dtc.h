@@ -119,7 +119,8 @@ int dtc_close(dtc_ctx* ctx);
 /* Free the ctx's batch work buffers (state batches, partial sums, kick
  * records; the next call re-allocates what it needs) after waiting for its
  * stream -- e.g. before the caller allocates one 256 GiB sharded state on the
- * same device.  The forward prefix (dtc_prefix_*) is kept. */
+ * same device.  The forward prefix (dtc_prefix_*) is kept: call
+ * dtc_prefix_release as well to free it (the Python wrapper does both). */
 int dtc_release_buffers(dtc_ctx* ctx);
 const char* dtc_last_error(void);
 int32_t dtc_abi_version(void);

@@ -1145,15 +1145,22 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   DTC_HIP(hipSetDevice(device));
   dtc_ctx* c = new dtc_ctx();
   c->device = device;
+#ifdef DTC_DEV_KNOBS
+  // development A/B builds only (make DEV=1): layout and launch-geometry
+  // overrides.  The product library ignores these variables, so a stray one
+  // cannot change the HBM layout or the kernels' geometry.
   if (const char* e = std::getenv("DTC_OCTET_BITS")) c->octet_bits = std::atoi(e);
   if (c->octet_bits != 0 && (c->octet_bits < 4 || c->octet_bits > 12)) c->octet_bits = 6;
   if (const char* e = std::getenv("DTC_LC_SPLIT")) c->lc_split = e[0] != '0';
   if (const char* e = std::getenv("DTC_LC_TPB")) c->lc_tpb = std::atoi(e);
   if (const char* e = std::getenv("DTC_KDK_SPLIT")) c->kdk_split = std::atoi(e);
   c->basis_synth = std::getenv("DTC_NO_BASIS_SYNTH") == nullptr;
+  if (const char* e = std::getenv("DTC_BATCH_BYTES")) c->batch_bytes = std::atof(e);
+#endif
+  // documented test switches (the parity tests compare the light-cone ends
+  // with the full passes, each form on its own engine)
   c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
   c->lc_wide = std::getenv("DTC_NO_LCW") == nullptr;
-  if (const char* e = std::getenv("DTC_BATCH_BYTES")) c->batch_bytes = std::atof(e);
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1208,6 +1215,7 @@ int dtc_release_buffers(dtc_ctx* ctx) {
   release(ctx->F);
   release(ctx->E);
   release(ctx->partial);
+  release(ctx->red_scratch);
   release(ctx->recs);
   release(ctx->recs1);
   release(ctx->pk);

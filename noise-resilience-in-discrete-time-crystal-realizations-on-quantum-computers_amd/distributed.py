@@ -74,6 +74,8 @@ def sharded_sweep(spec: SweepSpec, n_traj: int, shots=None, seed=0x5EED0001, bat
 
     from . import sweep as sw
 
+    if independent_t and want_zsite:
+        raise ValueError("independent_t: per-site Z is a forward-sweep output")  # as run_sweep
     world, rank = dist.get_world_size(), dist.get_rank()
     eng = engine or sw._default_engine()
     if shard == "auto":
@@ -108,8 +110,8 @@ def sharded_sweep(spec: SweepSpec, n_traj: int, shots=None, seed=0x5EED0001, bat
                 return empty(spec.n_inst, 0)
             if independent_t:
                 return sw.autocorr_independent_t(eng, spec, hi - lo, seed=seed, lo=lo,
-                                                 n_total=n_traj, want_fwd=want_fwd,
-                                                 want_echo=want_echo, batch=batch)
+                                                 want_fwd=want_fwd, want_echo=want_echo,
+                                                 batch=batch)
             return eng.autocorr(spec, hi - lo, seed=seed, traj_offset=lo, want_fwd=want_fwd,
                                 want_echo=want_echo, want_zsite=want_zsite, batch=batch)
 

@@ -332,9 +332,13 @@ class DtcEngine:
             ctypes.c_int32(period), ctypes.c_uint64(pre_mask), ctypes.c_int32(chunk_bits),
             ctypes.c_int32(slice_bits), ctypes.c_int32(slice_), ctypes.c_void_p(state_ptr)))
 
-    def release_buffers(self):
-        """Free the engine's batch work buffers (dtc_release_buffers); the
-        next call re-allocates what it needs."""
+    def release_buffers(self, drop_prefix: bool = True):
+        """Free the engine's batch work buffers (dtc_release_buffers) and, by
+        default, the forward prefix (dtc_prefix_release) -- all the engine's
+        large device memory, e.g. before one 256 GiB sharded state; the next
+        call re-allocates what it needs."""
+        if drop_prefix:
+            _capi.check(self._lib.dtc_prefix_release(self._ctx))
         _capi.check(self._lib.dtc_release_buffers(self._ctx))
 
     def shard_exchange_slice(self, shard, slice_bits: int, slice_: int, state_ptr: int):

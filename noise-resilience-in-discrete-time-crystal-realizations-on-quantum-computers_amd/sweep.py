@@ -74,19 +74,28 @@ def _shot_estimate(a: np.ndarray, shots: int, rng: np.random.Generator) -> np.nd
     return (2.0 * zero.sum(axis=1) - shots) / shots
 
 
+def point_seed(seed: int, t: int) -> int:
+    """The Philox key of time point t in the independent-per-t mode: a
+    splitmix64 finaliser of (seed, t), so every point draws from its own key
+    whatever trajectory ids a caller's chunks use."""
+    m = (1 << 64) - 1
+    z = (seed + (t + 1) * 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
 def autocorr_independent_t(eng, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
-                           lo: int = 0, n_total: int | None = None, want_fwd=True,
-                           want_echo=True, batch: int = 0) -> dict:
+                           lo: int = 0, want_fwd=True, want_echo=True, batch: int = 0) -> dict:
     """Per-trajectory outputs like ``eng.autocorr``, but every time point from
     its own trajectories, as the reference's fresh circuit per t
     (autocorr-delta-a-single-qiskit-fast.py:219-221): point t runs a sweep of
-    t + t_offset periods that measures only t (``t_first``), with trajectory ids
-    t * n_total + lo .. (+ n_traj) -- distinct Philox streams for every t, so
-    the points are uncorrelated across t and a run sharded over trajectory
-    blocks [lo, lo + n_traj) of n_total gives the same values.  Costs O(T^2)
+    t + t_offset periods that measures only t (``t_first``) under its own key
+    ``point_seed(seed, t)``, trajectory ids lo .. lo + n_traj - 1 -- so the
+    points share no noise draw across t, and chunks of one run split by
+    trajectory offset (``lo``) compose to the single-call values.  Costs O(T^2)
     period applications instead of O(T^2 / 2) shared with the forward branch:
     about 2 t periods per trajectory for point t."""
-    n_total = n_traj if n_total is None else n_total
     n_inst, T = spec.n_inst, spec.T
     out = {}
     if want_fwd:
@@ -96,7 +105,7 @@ def autocorr_independent_t(eng, spec: SweepSpec, n_traj: int, seed: int = 0x5EED
     for t in range(T):
         rows = max(1, t + spec.t_offset)
         s_t = dataclasses.replace(spec, T=t + 1, kick=spec.kick[:rows])
-        r = eng.autocorr(s_t, n_traj, seed=seed, traj_offset=t * n_total + lo,
+        r = eng.autocorr(s_t, n_traj, seed=point_seed(seed, t), traj_offset=lo,
                          want_fwd=want_fwd, want_echo=want_echo, batch=batch, t_first=t)
         for k in out:
             out[k][:, :, t] = r[k][:, :, t]

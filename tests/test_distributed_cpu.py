@@ -89,7 +89,7 @@ class _OracleEngine:
 
 def test_independent_t_points_are_their_own_trajectories(pkg):
     """--independent_t (the reference's fresh circuit per t, fast.py:219-221):
-    point t is the standard sweep's point t over trajectory ids t*n .. t*n+n-1
+    point t is the standard sweep's point t under its own key point_seed(77, t)
     (forward noise of periods 1..t and echo stream 1+t are those trajectories'),
     so the points share no noise draw across t; noiseless, it is the standard
     sweep exactly."""
@@ -99,10 +99,20 @@ def test_independent_t_points_are_their_own_trajectories(pkg):
     n = 3
     eng = _OracleEngine()
     got = pkg.sweep.autocorr_independent_t(eng, spec, n, seed=77)
+    keys = {pkg.sweep.point_seed(77, t) for t in range(spec.T)}
+    assert len(keys) == spec.T and 77 not in keys
     for t in range(spec.T):
-        ref = c_oracle.autocorr(spec, n, seed=77, traj_offset=t * n, n_threads=1)
+        ref = c_oracle.autocorr(spec, n, seed=pkg.sweep.point_seed(77, t), n_threads=1)
         for k in ("fwd", "echo"):
             assert np.abs(got[k][:, :, t] - ref[k][:, :, t]).max() < 1e-12, (k, t)
+    # chunks split by trajectory offset compose to the single call (ADVICE r3:
+    # the old t * n_total + lo ids made chunk 2's point 0 reuse chunk 1's point 1)
+    a = pkg.sweep.autocorr_independent_t(eng, spec, 2, seed=77)
+    b = pkg.sweep.autocorr_independent_t(eng, spec, 1, seed=77, lo=2)
+    for k in ("fwd", "echo"):
+        assert np.array_equal(np.concatenate([a[k], b[k]], axis=1), got[k])
+    with pytest.raises(ValueError):
+        pkg.sweep.run_sweep(spec, n_traj=1, engine=eng, independent_t=True, want_zsite=True)
     ideal = pkg.SweepSpec(L=spec.L, T=spec.T, hs=spec.hs, phis=spec.phis, g=0.95, use_noise=0,
                           initial_state="neel")
     a = pkg.sweep.run_sweep(ideal, n_traj=1, engine=eng, independent_t=True)
