@@ -10,7 +10,7 @@ HIPCFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-resul
 # geometry override variables (DTC_OCTET_BITS, DTC_LC_SPLIT, DTC_LC_TPB,
 # DTC_KDK_SPLIT, DTC_BATCH_BYTES, DTC_NO_BASIS_SYNTH); never the product
 ifeq ($(DEV),1)
-HIPCFLAGS += -DDTC_DEV_KNOBS
+HIPCFLAGS += -DDTC_DEV_KNOBS $(DEVFLAGS)
 endif
 # CPU oracle (test infrastructure): portable build, plus an x86-64-v3 build
 # that is loaded only on hosts with those features.
@@ -20,8 +20,8 @@ OBJDIR  := build/obj
 LIB     := $(PKG)/lib/libdtc_hip.so
 ORACLE  := oracle/liboracle.so
 ORACLE3 := oracle/liboracle_v3.so
-SRCS    := $(PKG)/csrc/dtc_kernels.hip $(PKG)/csrc/dtc_engine.cpp
-HDRS    := $(PKG)/csrc/dtc_kernels.h $(PKG)/csrc/dtc_rng.h include/dtc.h
+SRCS    := $(PKG)/csrc/dtc_kernels.hip $(PKG)/csrc/dtc_lightcone.hip $(PKG)/csrc/dtc_engine.cpp
+HDRS    := $(PKG)/csrc/dtc_kernels.h $(PKG)/csrc/dtc_device.h $(PKG)/csrc/dtc_rng.h include/dtc.h
 
 all: $(LIB) $(ORACLE) $(ORACLE3)
 
@@ -31,11 +31,15 @@ $(OBJDIR)/dtc_kernels.o: $(PKG)/csrc/dtc_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
 
+$(OBJDIR)/dtc_lightcone.o: $(PKG)/csrc/dtc_lightcone.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
+
 $(OBJDIR)/dtc_engine.o: $(PKG)/csrc/dtc_engine.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
 
-$(LIB): $(OBJDIR)/dtc_kernels.o $(OBJDIR)/dtc_engine.o
+$(LIB): $(OBJDIR)/dtc_kernels.o $(OBJDIR)/dtc_lightcone.o $(OBJDIR)/dtc_engine.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared $^ -o $@
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 7
+#define DTC_ABI_VERSION 9
 
 /* error codes */
 #define DTC_OK 0
@@ -223,6 +223,16 @@ int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise*
                          uint64_t pre_mask, int32_t chunk_bits, int32_t slice_bits,
                          int32_t slice, double* state);
 
+/* The last pre-exchange kicks of slice `slice` (as dtc_shard_kick_slice with
+ * chunk_bits = n_global) fused with its in-place exchange (as
+ * dtc_shard_exchange_slice): the pass of the last site group in pre_mask
+ * stores piece (r, c) at (c, r), so the exchange moves no bytes of its own
+ * (one GPU holding every shard; unitary kick kinds, else the two calls). */
+int dtc_shard_kick_exchange_slice(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                                  const dtc_shard* shard, uint64_t seed, int64_t traj,
+                                  int32_t period, uint64_t pre_mask, int32_t slice_bits,
+                                  int32_t slice, double* state);
+
 /* Virtual ranks only (one process holds every shard: n_shards = 2^n_global,
  * first_rank = 0): the period's all-to-all for slice `slice`, in place.  With
  * chunk bits = the top n_global local bits and slice bits = the next
@@ -306,6 +316,11 @@ int dtc_set_profiling(dtc_ctx* ctx, int32_t on);
 int dtc_kernel_stats(dtc_ctx* ctx, int32_t kind, int64_t* launches,
                      double* total_ms, double* total_bytes);
 int dtc_reset_stats(dtc_ctx* ctx);
+/* Light-cone ends launched since dtc_open, by kernel: counts[0] the 8-site
+ * window (dtc_lc_final*), [1] the 10-site window's generic kernel
+ * (dtc_lcw_final), [2] its three-re-layout C2 form (dtc_lcw2_final).
+ * Independent of profiling; lets tests assert which kernel a sweep ran. */
+int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [3] */);
 
 /* Device properties for reports. */
 int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,

@@ -118,6 +118,7 @@ struct dtc_ctx {
   bool verbose = false;      // DTC_VERBOSE
   int prefix_octet = 0;      // layout the prefix states were built in
   int64_t st_n[DTC_KERNEL_KINDS] = {};
+  int64_t lc_launches[3] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
   std::vector<Pending> pending;
@@ -540,7 +541,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
                      int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
                      const dtc::KickRec* recs = nullptr, int meas_parts = 0,
-                     int no_store = 0, const int64_t* basis = nullptr) {
+                     int no_store = 0, const int64_t* basis = nullptr, int swap_k = 0) {
   const int shape = pass_shape(ps);
   if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
   const int kind = pass_kind(rc, ps, shape);
@@ -635,7 +636,16 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     e1 = get_event(ctx);
     DTC_HIP(hipEventRecord(e0, ctx->stream));
   }
-  DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream));
+  int lc_variant = -1;
+  if (swap_k > 0) {
+    // the slice's last pre-exchange kick, stored at the partner piece
+    if (shape != dtc::kShapeK || meas_mode != dtc::kMeasNone || basis)
+      return fail(DTC_EINVAL, "internal: kick+exchange pass must be a plain kick pass");
+    DTC_HIP(dtc::launch_kick_swap(A, swap_k, kind, ctx->stream));
+  } else {
+    DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream, &lc_variant));
+  }
+  if (lc_variant >= 0 && lc_variant < 3) ++ctx->lc_launches[lc_variant];
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     // algorithmic bytes: a read and a store per amplitude, or one of them
@@ -860,6 +870,20 @@ void build_cone_tables(int L, int j, int n_inst, const double* h, const double* 
         const int e = part == 0 ? dtc::lc_pos5a(v) : v;  // storage swizzle of the j-5 .. j table
         o[2 * e] = std::cos(-0.5 * ang);
         o[2 * e + 1] = std::sin(-0.5 * ang);
+      }
+    }
+    // r = 4 split at j (dtc_lcw2_final): the product of the two is the r = 4
+    // table (dtc_kernels.h kLcTab4a / kLcTab4b; j - 4 >= 0 and j + 4 < L, the
+    // only geometry that kernel runs)
+    if (j - 4 >= 0 && j + 4 <= L - 1) {
+      for (int part = 0; part < 2; ++part) {
+        double* o = out.data() + ((size_t)in * dtc::kLcTab + (part == 0 ? dtc::kLcTab4a : dtc::kLcTab4b)) * 2;
+        for (int v = 0; v < 32; ++v) {
+          const double ang = part == 0 ? diag_angle(L, hh, pp, j - 3, j + 1, j - 4, j, j - 4, v)
+                                       : diag_angle(L, hh, pp, j + 1, j + 4, j, j + 4, j, v);
+          o[2 * v] = std::cos(-0.5 * ang);
+          o[2 * v + 1] = std::sin(-0.5 * ang);
+        }
       }
     }
   }
@@ -1236,6 +1260,12 @@ int dtc_reset_stats(dtc_ctx* ctx) {
     ctx->st_ms[k] = 0;
     ctx->st_bytes[k] = 0;
   }
+  return DTC_OK;
+}
+
+int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts) {
+  if (!ctx || !counts) return fail(DTC_EINVAL, "null ctx / counts");
+  for (int k = 0; k < 3; ++k) counts[k] = ctx->lc_launches[k];
   return DTC_OK;
 }
 
@@ -2284,6 +2314,61 @@ int dtc_shard_kick_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* n
                            (uint32_t)period, skip_bits(G, pre_mask)};
     DTC_TRY(launch_pass_spec(ctx, rc, 0, (int)n_pieces, ps, base, base, dtc::kMeasNone, 1, 2,
                              nullptr, 0));
+  }
+  return DTC_OK;
+}
+
+int dtc_shard_kick_exchange_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                                  const dtc_shard* sh, uint64_t seed, int64_t traj,
+                                  int32_t period, uint64_t pre_mask, int32_t slice_bits,
+                                  int32_t slice, double* state) {
+  if (!ctx || !sh || !state) return fail(DTC_EINVAL, "null ctx/shard/state");
+  const int k = sh->n_global, nl = sh->n_local;
+  if (sh->n_shards != (1 << k) || sh->first_rank != 0)
+    return fail(DTC_EINVAL, "the in-place exchange needs every shard in this buffer");
+  DTC_TRY(shard_check_common(ctx, pr, nz, sh, traj, 0));
+  if (slice_bits < 0 || k + slice_bits > 16 || nl - k - slice_bits < dtc::kTileBits)
+    return fail(DTC_EINVAL, "chunk_bits + slice_bits must leave >= 12 bits per slice");
+  if (slice < 0 || slice >= (1 << slice_bits)) return fail(DTC_EINVAL, "slice out of range");
+  const int nsub = nl - k - slice_bits;
+  const uint64_t low = (1ull << nsub) - 1;
+  if (pre_mask & ~low) return fail(DTC_EINVAL, "slice kick mask reaches the chunk/slice bits");
+  RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
+  const Plan& pl = rc.pl;
+  // the group whose pass goes last carries the exchange (a unitary kick kind)
+  int last = -1;
+  for (size_t g = 0; g < pl.groups.size(); ++g)
+    if (pre_mask & group_bits(pl.groups[g])) last = (int)g;
+  bool fuse = last >= 0;
+  if (fuse) {
+    PassSpec ps{last, no_kick(), no_kick(), dtc::kDiagNone, 0};
+    ps.pre = dtc::KickDesc{1, 0, dtc::kKickForward, dtc::kStreamForward, 1u, 0u};
+    const int kind = pass_kind(rc, ps, dtc::kShapeK);
+    fuse = kind == dtc::kKindRX || kind == dtc::kKindRY || kind == dtc::kKindGen;
+  }
+  if (!fuse) {
+    DTC_TRY(dtc_shard_kick_slice(ctx, pr, nz, sh, seed, traj, period, pre_mask, k, slice_bits,
+                                 slice, state));
+    return dtc_shard_exchange_slice(ctx, sh, slice_bits, slice, state);
+  }
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  if (period < 1 || period > n_rows) return fail(DTC_EINVAL, "period outside kick table");
+  DTC_HIP(hipSetDevice(ctx->device));
+  DTC_TRY(shard_kick_tables(ctx, pr, sh, rc));
+  rc.L_eff_override = nsub;
+  rc.stride_override = (int64_t)1 << (nl - k);
+  double2* base = (double2*)state + ((size_t)slice << nsub);
+  const int n_pieces = 1 << (2 * k);
+  for (size_t g = 0; g < pl.groups.size(); ++g) {
+    const Group& G = pl.groups[g];
+    const uint64_t gb = group_bits(G);
+    if (!(pre_mask & gb)) continue;
+    if (gb & ~low) return fail(DTC_EINVAL, "a site group of the kick mask reaches the slice bits");
+    PassSpec ps{(int)g, no_kick(), no_kick(), dtc::kDiagNone, 0};
+    ps.pre = dtc::KickDesc{1, period - 1, dtc::kKickForward, dtc::kStreamForward,
+                           (uint32_t)period, skip_bits(G, pre_mask)};
+    DTC_TRY(launch_pass_spec(ctx, rc, 0, n_pieces, ps, base, base, dtc::kMeasNone, 1, 2, nullptr,
+                             0, nullptr, 0, 0, nullptr, (int)g == last ? k : 0));
   }
   return DTC_OK;
 }

@@ -89,7 +89,13 @@ __host__ __device__ constexpr int lc_pos4(int i) { return i ^ ((i >> 8) & 1); }
 __host__ __device__ constexpr int lc_pos5a(int i) { return i ^ ((i >> 4) & 3); }
 static constexpr int kLcTab5a = kLcTab4;
 static constexpr int kLcTab5b = kLcTab4 + 64;
-static constexpr int kLcTab = kLcTab4 + 128;  // per-instance stride of PassArgs::lc_diag
+// The radius-4 cone diagonal split at j like r = 5 (dtc_lcw2_final): bits
+// j-4 .. j (fields j-3 .. j, bonds (j-4, j-3) .. (j-1, j)) and bits j .. j+4
+// (fields j+1 .. j+3, bonds (j, j+1) .. (j+3, j+4)), natural order, so the
+// kernel's tables fit four workgroups per CU.
+static constexpr int kLcTab4a = kLcTab4 + 128;
+static constexpr int kLcTab4b = kLcTab4 + 160;
+static constexpr int kLcTab = kLcTab4 + 192;  // per-instance stride of PassArgs::lc_diag
 // kShapeLC with lc_wide: six kick layers over a 10-site window (one more
 // pass of the echo chain merged).  Tile bits 0, 1 = global bits 0, 1 (64-B
 // runs), tile bits 2 .. 11 = window sites lc_gb[2 .. 11] (host-chosen: nibble
@@ -262,7 +268,15 @@ __host__ __device__ __forceinline__ int64_t octet_padded(int64_t n, int g) {
 hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
 
 // act must cover nibble sets {2}, {1,2} or {0,1,2}; L_eff in [12, 32].
-hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);
+// lc_variant (kShapeLC passes, nullable): which light-cone kernel ran
+// (kLcVariant* below)
+hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream,
+                       int* lc_variant = nullptr);
+
+// kShapeLC passes (dtc_lightcone.hip), from launch_pass with its grid
+enum LcVariant { kLcVariant8 = 0, kLcVariantWide = 1, kLcVariantWide2 = 2 };
+hipError_t launch_lightcone(const PassArgs& a, dim3 grid, int kind, hipStream_t stream,
+                            int* variant);
 
 // out[b * out_stride + o] = sum over tiles of partial[b][tile][o_first + o],
 // o < n_out (fixed order); accumulate: += instead of =.  Large states
@@ -279,6 +293,12 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
 // batch layout of octet_bits (state_base / octet_spread)
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx,
                             int batch, hipStream_t stream, int octet_bits = 0);
+
+// A kick-only pass over the W^2 slice pieces of 2^k_bits shards (batch
+// b = r W + c, contiguous, in place) that stores piece (r, c) at (c, r): the
+// slice's last pre-exchange kick fused with the in-place all-to-all below.
+// Unitary kick kinds (RX, RY, general) only.
+hipError_t launch_kick_swap(const PassArgs& a, int k_bits, int kind, hipStream_t stream);
 
 // Virtual ranks' in-place all-to-all of one slice: 2^k shards of 2^nl
 // amplitudes, chunk = top k local bits, slice = the next nl - k - nsub bits;

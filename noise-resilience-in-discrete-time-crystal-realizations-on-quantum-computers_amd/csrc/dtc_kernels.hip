@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "dtc_device.h"
 #include "dtc_kernels.h"
 #include "dtc_rng.h"
 
@@ -44,24 +45,6 @@
 #endif
 
 namespace dtc {
-
-typedef double d2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-
-// General: (u, v) <- (m00 u + m01 v, m10 u + m11 v)
-__device__ __forceinline__ void bfly_general(double2& u, double2& v, const double2* m) {
-  const double2 m00 = m[0], m01 = m[1], m10 = m[2], m11 = m[3];
-  double2 nu, nv;
-  nu.x = m00.x * u.x - m00.y * u.y + m01.x * v.x - m01.y * v.y;
-  nu.y = m00.x * u.y + m00.y * u.x + m01.x * v.y + m01.y * v.x;
-  nv.x = m10.x * u.x - m10.y * u.y + m11.x * v.x - m11.y * v.y;
-  nv.y = m10.x * u.y + m10.y * u.x + m11.x * v.y + m11.y * v.x;
-  u = nu;
-  v = nv;
-}
 
 // m <- P m for Pauli code (1 X, 2 Y, 3 Z)
 __device__ __forceinline__ void pauli_left(double2* m, int pauli) {
@@ -393,344 +376,6 @@ hipError_t launch_prep(const PrepArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// Tile layouts: register r of lane-thread t holds tile index Y(t, r) =
-// ybase<LAY>(t) | (r << 4 LAY).
-// Layout 2: registers = tile bits 8..11, threads = bits 0..7 (coalesced).
-// Layout 1: registers = tile bits 4..7.  Layout 0: registers = bits 0..3.
-template <int LAY>
-__device__ __forceinline__ int ybase(int t) {
-  if (LAY == 2) return t;
-  if (LAY == 1) return (t & 15) | ((t >> 4) << 8);
-  return t << 4;
-}
-template <int LAY>
-__device__ __forceinline__ int tile_y(int t, int r) {
-  return ybase<LAY>(t) | (r << (4 * LAY));
-}
-
-// XOR swizzle over 16-B slots: conflict-free ds_write_b128 / ds_read_b128 for
-// every layout transition used here (MI355X_MICROARCH.md §LDS lane groups).
-__device__ __forceinline__ int lds_slot(int y) { return y ^ ((y >> 4) & 15); }
-
-// Factored RX-family butterfly (see SiteMat): (u, v) <- diag(1, sigma) S (u, v)
-template <int VAR>
-__device__ __forceinline__ void bfly_rx_f(double2& u, double2& v, double f) {
-  double2 nu, nv;
-  if (VAR == 0) {  // S = [[1, i f], [i f, 1]]
-    nu.x = fma(-f, v.y, u.x); nu.y = fma(f, v.x, u.y);
-    nv.x = fma(-f, u.y, v.x); nv.y = fma(f, u.x, v.y);
-  } else if (VAR == 1) {  // sigma = -1
-    nu.x = fma(-f, v.y, u.x); nu.y = fma(f, v.x, u.y);
-    nv.x = fma(f, u.y, -v.x); nv.y = fma(-f, u.x, -v.y);
-  } else if (VAR == 2) {  // S = [[f, i], [i, f]]
-    nu.x = fma(f, u.x, -v.y); nu.y = fma(f, u.y, v.x);
-    nv.x = fma(f, v.x, -u.y); nv.y = fma(f, v.y, u.x);
-  } else {
-    nu.x = fma(f, u.x, -v.y); nu.y = fma(f, u.y, v.x);
-    nv.x = fma(-f, v.x, u.y); nv.y = fma(-f, v.y, -u.x);
-  }
-  u = nu;
-  v = nv;
-}
-
-// Factored RY-family butterfly: (u, v) <- diag(1, sigma) R (u, v)
-template <int VAR>
-__device__ __forceinline__ void bfly_ry_f(double2& u, double2& v, double f) {
-  double2 nu, nv;
-  if (VAR == 0) {  // R = [[1, f], [-f, 1]]
-    nu.x = fma(f, v.x, u.x); nu.y = fma(f, v.y, u.y);
-    nv.x = fma(-f, u.x, v.x); nv.y = fma(-f, u.y, v.y);
-  } else if (VAR == 1) {
-    nu.x = fma(f, v.x, u.x); nu.y = fma(f, v.y, u.y);
-    nv.x = fma(f, u.x, -v.x); nv.y = fma(f, u.y, -v.y);
-  } else if (VAR == 2) {  // R = [[f, 1], [-1, f]]
-    nu.x = fma(f, u.x, v.x); nu.y = fma(f, u.y, v.y);
-    nv.x = fma(f, v.x, -u.x); nv.y = fma(f, v.y, -u.y);
-  } else {
-    nu.x = fma(f, u.x, v.x); nu.y = fma(f, u.y, v.y);
-    nv.x = fma(-f, v.x, u.x); nv.y = fma(-f, v.y, u.y);
-  }
-  u = nu;
-  v = nv;
-}
-
-template <int KIND, int VAR, int Q>
-__device__ __forceinline__ void layer_f(double2 (&v)[kRegs], double f) {
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) {
-    if (r & (1 << Q)) continue;
-    if (KIND == kKindRX) bfly_rx_f<VAR>(v[r], v[r | (1 << Q)], f);
-    else bfly_ry_f<VAR>(v[r], v[r | (1 << Q)], f);
-  }
-}
-
-// The kick records of a (pass, state) — 25 x 64 B — live in the VGPRs of
-// every wave: lane l holds doubles [4l, 4l + 4) of the block (loaded with the
-// setup, before the tile); a coefficient is two v_readlane_b32 with static
-// lane and register indices: no LDS, no scalar-memory round trip per layer.
-struct RecRegs {
-  double rv[4];
-  __device__ __forceinline__ long long bits(int j) const {
-    const long long x = __double_as_longlong(rv[j & 3]);
-    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), j >> 2);
-    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), j >> 2);
-    return ((long long)hi << 32) | (unsigned int)lo;
-  }
-  __device__ __forceinline__ double d(int rec, int e) const {
-    return __longlong_as_double(bits(8 * rec + e));
-  }
-  __device__ __forceinline__ int i(int rec, int e) const { return (int)bits(8 * rec + e); }
-};
-
-template <int N, int KIND>
-__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs& R, int rec0) {
-  // Every site of an active nibble runs (inactive sites carry the identity):
-  // no data-dependent branches, so no register shuffles at merge points; the
-  // RX/RY variant branch is wave-uniform.
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = rec0 + 4 * N + q;
-    if (KIND == kKindGen) {
-      double2 m[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = make_double2(R.d(k, 2 * e), R.d(k, 2 * e + 1));
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r)
-        if (!(r & (1 << q))) bfly_general(v[r], v[r | (1 << q)], m);
-    } else if (KIND == kKindRXU || KIND == kKindRYU) {
-      // S of form A or B only (the sign and the Kraus factor: the deferred
-      // diag(1, rho), rho_apply)
-      constexpr int BK = KIND == kKindRXU ? kKindRX : kKindRY;
-      const double f = R.d(k, 0);
-      const int var = R.i(k, 1);
-      auto run = [&](auto qtag) {
-        constexpr int Q = decltype(qtag)::value;
-        if (var == 0) layer_f<BK, 0, Q>(v, f);
-        else layer_f<BK, 2, Q>(v, f);
-      };
-      if (q == 0) run(std::integral_constant<int, 0>{});
-      else if (q == 1) run(std::integral_constant<int, 1>{});
-      else if (q == 2) run(std::integral_constant<int, 2>{});
-      else run(std::integral_constant<int, 3>{});
-    } else {
-      const double f = R.d(k, 0);
-      const int var = R.i(k, 1);
-      auto run = [&](auto qtag) {
-        constexpr int Q = decltype(qtag)::value;
-        if (var == 0) layer_f<KIND, 0, Q>(v, f);
-        else if (var == 1) layer_f<KIND, 1, Q>(v, f);
-        else if (var == 2) layer_f<KIND, 2, Q>(v, f);
-        else layer_f<KIND, 3, Q>(v, f);
-      };
-      if (q == 0) run(std::integral_constant<int, 0>{});
-      else if (q == 1) run(std::integral_constant<int, 1>{});
-      else if (q == 2) run(std::integral_constant<int, 2>{});
-      else run(std::integral_constant<int, 3>{});
-    }
-  }
-}
-
-// Tile re-layout through LDS.  No barrier before the writes: a thread writes
-// exactly the slots it read itself in the previous exchange (that one ended in
-// layout FROM), so no other thread can still need them.
-template <int FROM, int TO>
-__device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, int t) {
-  if (FROM == TO) return;
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y<FROM>(t, r))] = v[r];
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y<TO>(t, r))];
-}
-
-// The same re-layout through a 32 KiB buffer, real parts then imaginary parts
-// (8-B slots, swizzle y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4), half-wave
-// conflict-free): half the LDS, so three workgroups fit a CU; two more
-// barriers (the imaginary writes reuse the slots the real reads just left).
-__device__ __forceinline__ int lds_slot8(int y) { return y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4); }
-// lds_slot8(tile_y<LAY>(t, r)) = slot8_of<LAY>(lds_slot8(ybase<LAY>(t)), r): the
-// register part is a compile-time XOR (layouts 0, 1) or an XOR of bit 4 plus an
-// offset (layout 2) on a per-thread base
-template <int LAY>
-__device__ __forceinline__ int slot8_of(int base, int r) {
-  if (LAY == 0) return base ^ r;
-  if (LAY == 1) return base ^ (17 * r);
-  return (base ^ ((r & 1) << 4)) | (r << 8);
-}
-template <int FROM, int TO>
-__device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t) {
-  if (FROM == TO) return;
-  // the two per-thread bases are made opaque here, so every exchange forms its
-  // slots afresh (one XOR each) instead of the compiler keeping 16 slot
-  // addresses per layout live across the kernel (48 VGPRs: the 12-site K-D-K
-  // at three workgroups per CU spilled 80 B/lane for them, r3h PMC: +24 % HBM
-  // writes)
-  int bf = lds_slot8(ybase<FROM>(t)), bt = lds_slot8(ybase<TO>(t));
-  asm volatile("" : "+v"(bf), "+v"(bt));
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_half[slot8_of<FROM>(bf, r)] = v[r].x;
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r].x = s_half[slot8_of<TO>(bt, r)];
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_half[slot8_of<FROM>(bf, r)] = v[r].y;
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r].y = s_half[slot8_of<TO>(bt, r)];
-}
-
-template <bool SPLIT, int FROM, int TO>
-__device__ __forceinline__ void xch_tile(double2 (&v)[kRegs], double2* s_tile, double* s_half,
-                                         int t) {
-  if constexpr (SPLIT) exchange_split<FROM, TO>(v, s_half, t);
-  else exchange<FROM, TO>(v, s_tile, t);
-}
-
-__device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chunks, int64_t x) {
-  double2 ph = s_chunk[x & 63];
-  for (int k = 1; k < n_chunks; ++k) {
-    ph = cmul(ph, s_chunk[k * 64 + ((x >> (kChunkBits * k)) & 63)]);
-  }
-  return ph;
-}
-
-// Value of lane (l ^ M) for every lane l, M = 1 .. 32, without LDS: DPP
-// quad permutes (1, 2) and row rotations (4, 8) on the VALU, and gfx950's
-// v_permlane16_swap / v_permlane32_swap (16, 32).  A row rotation by n gives
-// lane l the value of lane ((l - n) mod 16); l ^ 8 is one such rotation, l ^ 4
-// is (l + 4) or (l - 4) by lane bit 2.  permlane{16,32}_swap(x, x) returns
-// (x with its even rows/lower half copied up, x with its odd rows/upper half
-// copied down): the xor partner is the first for lanes with the bit set.
-template <int M>
-__device__ __forceinline__ int xor_lane_b32(int x) {
-  static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor");
-  if constexpr (M == 1) {
-    return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  } else if constexpr (M == 2) {
-    return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  } else if constexpr (M == 8) {
-    return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
-  } else if constexpr (M == 4) {
-    const int up = __builtin_amdgcn_update_dpp(0, x, 0x12C, 0xF, 0xF, false);  // l - 12 = l + 4
-    const int dn = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // l - 4
-    return (__lane_id() & 4) ? dn : up;
-  } else if constexpr (M == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return (__lane_id() & 16) ? (int)r[0] : (int)r[1];
-  } else {
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return (__lane_id() & 32) ? (int)r[0] : (int)r[1];
-  }
-}
-
-template <int M>
-__device__ __forceinline__ double xor_lane(double x) {
-  const long long b = __double_as_longlong(x);
-  const int lo = xor_lane_b32<M>((int)(b & 0xffffffffll));
-  const int hi = xor_lane_b32<M>((int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ double wave_sum(double x) {
-  x += xor_lane<32>(x);
-  x += xor_lane<16>(x);
-  x += xor_lane<8>(x);
-  x += xor_lane<4>(x);
-  x += xor_lane<2>(x);
-  x += xor_lane<1>(x);
-  return x;
-}
-
-// One butterfly stage of a Walsh-Hadamard transform over the wave's lanes:
-// lane l ends with h(l) + h(l ^ M) or h(l ^ M) - h(l) by lane bit M.
-template <int M>
-__device__ __forceinline__ double wht_stage(double h) {
-  const double o = xor_lane<M>(h);
-  return fma((__lane_id() & M) ? -1.0 : 1.0, h, o);
-}
-
-// permlane{32,16}_swap of a pair of doubles (both 32-bit halves): with
-// vdst = a, src0 = b, a becomes (a's lower half-wave / even rows, b's lower /
-// even) and b becomes (a's upper / odd, b's upper / odd).  For a pair whose
-// first member is kept by the lanes without the bit and the second by the
-// lanes with it, a + b afterwards is, in every lane, its kept vector summed
-// with the partner lane's copy: one swap pair and one add per stage, no
-// selects, no copies.
-template <int M>
-__device__ __forceinline__ void swap_rows(double& a, double& b) {
-  const long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
-  const int alo = (int)(ab & 0xffffffffll), ahi = (int)(ab >> 32);
-  const int blo = (int)(bb & 0xffffffffll), bhi = (int)(bb >> 32);
-  if constexpr (M == 32) {
-    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
-    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
-    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
-  } else {
-    static_assert(M == 16, "row swap");
-    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
-    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
-    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
-  }
-}
-
-// Sum of NV per-lane vectors over the wave (NV = 4 or 8), halving the vector
-// count per lane at each of the first stages: afterwards every lane of the
-// group of 8 with lane bits (5, 4, 3) = v (NV = 8; NV = 4: bits (5, 4)
-// and every bit-3 value) holds the wave sum of vector v.
-template <int NV>
-__device__ __forceinline__ double wave_sum_multi(const double (&x)[NV]) {
-  const int lane = __lane_id();
-  double a[NV / 2];
-#pragma unroll
-  for (int m = 0; m < NV / 2; ++m) {
-    double u = x[m], w = x[NV / 2 + m];
-    swap_rows<32>(u, w);
-    a[m] = u + w;
-  }
-  double b[NV / 4];
-#pragma unroll
-  for (int m = 0; m < NV / 4; ++m) {
-    double u = a[m], w = a[NV / 4 + m];
-    swap_rows<16>(u, w);
-    b[m] = u + w;
-  }
-  double c;
-  if constexpr (NV == 8) {
-    const bool h3 = lane & 8;
-    c = (h3 ? b[1] : b[0]) + xor_lane<8>(h3 ? b[0] : b[1]);
-  } else {
-    c = b[0] + xor_lane<8>(b[0]);
-  }
-  c += xor_lane<4>(c);
-  c += xor_lane<2>(c);
-  c += xor_lane<1>(c);
-  return c;
-}
-
-// Lane patterns kept from a wave's Walsh-Hadamard transform (s_red entries):
-// 0, the single bits 1 .. 32 and the adjacent pairs 3 .. 48 — every site or
-// bond observable needs one of them.  -1: not kept.
-__device__ __forceinline__ int lane_pattern(int m) {
-  if (m == 0) return 0;
-  const int k = __ffs(m) - 1;
-  if (m == (1 << k)) return 1 + k;
-  if (k < 5 && m == (3 << k)) return 7 + k;
-  return -1;
-}
-
-// Per-layout global index of register r: x(r) = x0(t) | off(r), off uniform.
-struct TileMap {
-  int64_t tbase;
-  int c, s, cmask;
-  __device__ __forceinline__ int64_t rel(int y) const {
-    return (int64_t)(y & cmask) | ((int64_t)(y >> c) << s);
-  }
-  __device__ __forceinline__ int64_t at(int y) const { return tbase | rel(y); }
-};
-
 // Compile-time round plan.  NIBS = register nibbles holding active sites
 // (bit n = nibble n).  IO = the load/store layout (io_layout), O = 3 - IO the
 // other high nibble.
@@ -775,7 +420,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
 #endif
   DTC_TS(0);
   __shared__ double2 s_tile[SPLIT ? 1 : kTile];
-  __shared__ double s_half[SPLIT ? kTile : 1];
+  __shared__ double s_half[SPLIT ? kHalfSlots : 1];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
   __shared__ double s_red[kThreads / 64][kRedSlots];
@@ -1392,465 +1037,6 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
   pass_body<kShapeD, NIBS, kKindRX, MC>(A);
 }
 
-static constexpr int kLcTilesPerGroup = 2;
-
-// ---- the light-cone end of an echo chain (kShapeLC) ------------------------
-// The chain ends with <Z_j>.  Going backward from the measurement, the last
-// kick layer matters only on j, the one before on j-1..j+1, the r-th from the
-// end on j-r..j+r (kicks are unitary and D is diagonal with nearest-neighbour
-// terms), so the chain's last few passes collapse into one measure-only pass
-// over tiles that hold the window w0..w0+7 (tile bits 4..11; bits 0..3 =
-// sites 0..3 as columns, c = 4): layer l = 0 .. lc_layers-1 kicks the window
-// sites its mask keeps -- nibble 2 then 1 for even l, 1 then 2 for odd l, one
-// LDS re-layout between them -- with the cone diagonal (conjugated: echo)
-// between consecutive layers; then the probe.  Kicks in Pauli-frame form
-// (dtc_kernels.h): one butterfly variant; a site of a layer runs only when the
-// layer's mask kicks it (scalar branches on the kernel argument).
-// A workgroup takes TPB consecutive tiles of one state: the records and tables
-// are staged once, and the next tile's 16 loads are issued before the current
-// tile's layers (register double buffer: the pass is VALU/LDS-heavy per byte).
-template <int KIND, int TPB, bool SPLIT = false>
-__device__ __forceinline__ void lc_body(const PassArgs& A) {
-  static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
-  __shared__ double2 s_tile[SPLIT ? 1 : kTile];
-  __shared__ double s_half[SPLIT ? kTile : 1];
-  __shared__ double2 s_cone[kLcTab4];
-  __shared__ double s_red[kThreads / 64][2];
-  const int t = threadIdx.x;
-  const int c = A.c, s = A.s;  // c = 4, s = w0
-  const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
-  const int og = A.octet_bits;  // state layout, as pass_body
-  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
-  const int64_t tile0 = (og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x) * TPB;
-  if (og && b >= A.batch) return;
-  const int inst = (int)((A.batch_start + b) / A.n_traj);
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcPacked + 1) {  // the records: lanes 0 .. 10
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
-  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
-  TileMap M;
-  M.c = c;
-  M.s = s;
-  M.cmask = (1 << c) - 1;
-  auto tbase_of = [&](int64_t tile) {
-    return ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
-  };
-  M.tbase = tbase_of(tile0);
-  constexpr int kConePerThread = (kLcTab4 + kThreads - 1) / kThreads;
-  double2 cv[kConePerThread];
-  const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
-#pragma unroll
-  for (int j = 0; j < kConePerThread; ++j) {
-    const int i = t + j * kThreads;
-    if (i < kLcTab4) cv[j] = ct[i];
-  }
-  // the tile in layout 2 (threads = tile bits 0..7: 16-amplitude runs)
-  // (layout 2: lanes = tile bits 0..3 (columns) and window sites 0..3; a
-  // 64-bit lane offset: the window may sit high in a large state)
-  const int64_t vofs = octet_spread(M.rel(ybase<2>(t)), og) << 4;
-  const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
-  auto load_tile = [&](double2 (&dst)[kRegs], int64_t tb) {
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      const char* a = src + (octet_spread(tb | M.rel(r << 8), og) << 4) + vofs;
-      const d2v w = __builtin_nontemporal_load((const d2v*)a);
-      dst[r] = make_double2(w.x, w.y);
-    }
-  };
-  double2 v[kRegs];
-  load_tile(v, M.tbase);
-  __builtin_amdgcn_s_waitcnt(0x4F70);  // records and tables landed, the tile's 16 loads in flight
-  const double cs = A.diag_conj ? -1.0 : 1.0;
-#pragma unroll
-  for (int j = 0; j < kConePerThread; ++j) {
-    const int i = t + j * kThreads;
-    if (i < kLcTab4) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
-  }
-  // (visible after the first re-layout's barrier)
-  const double g2 = R.d(0, kLcG2);
-  const long long packed = R.bits(kLcPacked);
-  const int nl = A.lc_layers;
-  const int jp = A.probe;
-
-  // kicks of nibble N (window sites 4 (N-1) .. 4 (N-1) + 3) in layer l
-  auto kick = [&](double2 (&v)[kRegs], auto n_tag, auto l_tag) {
-    constexpr int N = decltype(n_tag)::value;
-    constexpr int l = decltype(l_tag)::value;
-    constexpr int k0 = kLcSites * l + 4 * (N - 1);
-    // per site: the cone leaves most layers' nibbles partly idle (the last
-    // layer kicks j alone), and an idle site's f = 0 butterfly is the
-    // identity; the mask is a kernel argument, so these are scalar branches
-    const int m = (int)((A.lc_mask >> k0) & 0xFull);
-    if (m & 1) layer_f<KIND, 0, 0>(v, R.d(0, k0));
-    if (m & 2) layer_f<KIND, 0, 1>(v, R.d(0, k0 + 1));
-    if (m & 4) layer_f<KIND, 0, 2>(v, R.d(0, k0 + 2));
-    if (m & 8) layer_f<KIND, 0, 3>(v, R.d(0, k0 + 3));
-  };
-  // cone diagonal after layer l, applied in layout LAY: D_r(x ^ m_l), one
-  // table lookup and one complex product per amplitude
-  auto diag = [&](double2 (&v)[kRegs], auto lay_tag, int l) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int rad = nl - 1 - l;
-    const int lo = max(0, jp - rad), hi = min(A.L_real - 1, jp + rad);
-    const int msk = (1 << (hi - lo + 1)) - 1;
-    const int g0 = s + 4 * LAY - c;  // global bit of register bit 0
-    const int64_t m = (int64_t)((packed >> (8 * l)) & 0xFF) << s;
-    const int base = (int)(((M.at(ybase<LAY>(t)) ^ m) >> lo) & msk);
-    const double2* tab = s_cone + lc_tab_off(rad);
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      const int off = (g0 >= lo ? (r << (g0 - lo)) : (r >> (lo - g0))) & msk;
-      const int i = base ^ off;
-      v[r] = cmul(v[r], tab[rad == 4 ? lc_pos4(i) : i]);  // (the radius-4 table's storage)
-    }
-  };
-  using L1 = std::integral_constant<int, 1>;
-  using L2 = std::integral_constant<int, 2>;
-  auto lc_xch_impl = [&](double2 (&v)[kRegs], auto from_tag, auto to_tag) {
-    constexpr int F = decltype(from_tag)::value, T = decltype(to_tag)::value;
-    if constexpr (SPLIT) exchange_split<F, T>(v, s_half, t);
-    else exchange<F, T>(v, s_tile, t);
-  };
-  // one tile, its amplitudes in v (layout 2)
-  auto process = [&](double2 (&v)[kRegs], int64_t tile) {
-    M.tbase = tbase_of(tile);
-    // layer 0: nibble 2 (layout 2), re-layout, nibble 1 (layout 1), D
-    kick(v, L2{}, std::integral_constant<int, 0>{});
-    lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-    kick(v, L1{}, std::integral_constant<int, 0>{});
-    if (nl > 1) {  // layer 1: 1 -> 2
-      diag(v, L1{}, 0);
-      kick(v, L1{}, std::integral_constant<int, 1>{});
-      lc_xch_impl(v, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-      kick(v, L2{}, std::integral_constant<int, 1>{});
-    }
-    if (nl > 2) {  // layer 2: 2 -> 1
-      diag(v, L2{}, 1);
-      kick(v, L2{}, std::integral_constant<int, 2>{});
-      lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-      kick(v, L1{}, std::integral_constant<int, 2>{});
-    }
-    if (nl > 3) {  // layer 3: 1 -> 2
-      diag(v, L1{}, 2);
-      kick(v, L1{}, std::integral_constant<int, 3>{});
-      lc_xch_impl(v, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-      kick(v, L2{}, std::integral_constant<int, 3>{});
-    }
-    if (nl > 4) {  // layer 4: 2 -> 1
-      diag(v, L2{}, 3);
-      kick(v, L2{}, std::integral_constant<int, 4>{});
-      lc_xch_impl(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-      kick(v, L1{}, std::integral_constant<int, 4>{});
-    }
-    // probe: layout 1 after an odd number of layers, 2 after an even number;
-    // the frame's X on j flips it
-    const int lay = (nl & 1) ? 1 : 2;
-    double ptot = 0.0, pz = 0.0;
-    {
-      const int64_t x0 = lay == 1 ? M.at(ybase<1>(t)) : M.at(ybase<2>(t));
-      const int tb = jp < c ? jp : ((jp >= s && jp < s + kTileBits - c) ? c + jp - s : -1);
-      const int jr = tb - 4 * lay;  // register bit of the probe, if in the nibble in registers
-#pragma unroll
-      for (int r = 0; r < kRegs; ++r) {
-        const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
-        ptot += p2;
-        pz += (jr >= 0 && jr < 4 && ((r >> jr) & 1)) ? -p2 : p2;
-      }
-      if (!(jr >= 0 && jr < 4)) pz = ((x0 >> jp) & 1) ? -ptot : ptot;
-      if ((packed >> (32 + jp - s)) & 1) pz = -pz;
-    }
-    const int wave = t >> 6, lane = t & 63;
-    const double tot = wave_sum(ptot) * g2;
-    const double z = wave_sum(pz) * g2;
-    if (lane == 0) {
-      s_red[wave][0] = tot;
-      s_red[wave][1] = z;
-    }
-    __syncthreads();
-    if (t < 2) {
-      double acc = 0.0;
-      for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
-      A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
-    }
-  };
-  // two register buffers, no copies: the loads of tile i+1 fly while tile i runs
-  static_assert(TPB == 1 || TPB == 2 || TPB == 4, "tiles per workgroup");
-  if constexpr (TPB == 1) {
-    process(v, tile0);
-  } else {
-    double2 w[kRegs];
-    load_tile(w, tbase_of(tile0 + 1));
-    process(v, tile0);
-    if constexpr (TPB == 4) {
-      load_tile(v, tbase_of(tile0 + 2));
-      process(w, tile0 + 1);
-      load_tile(w, tbase_of(tile0 + 3));
-      process(v, tile0 + 2);
-      process(w, tile0 + 3);
-    } else {
-      process(w, tile0 + 1);
-    }
-  }
-}
-
-template <int KIND, int TPB>
-__global__ __launch_bounds__(kThreads, 2) void dtc_lc_final(PassArgs A) {
-  lc_body<KIND, TPB>(A);
-}
-// One tile per workgroup, re-layouts through half the LDS: three per CU (the
-// pass is bound by its per-workgroup chain, so a third chain per CU pays more
-// than the two extra barriers per re-layout cost; the default)
-template <int KIND>
-__global__ __launch_bounds__(kThreads, 3) void dtc_lc_final_split(PassArgs A) {
-  lc_body<KIND, 1, true>(A);
-}
-
-// ---- the 10-site light-cone end (kShapeLC, lc_wide) ------------------------
-// The chain's last five passes as six kick layers (r = 5 .. 0 diagonals before
-// the probe) on a 10-site window (dtc_kernels.h, kLcw*).  Tile bits 0, 1 =
-// global bits 0, 1 (64-B runs), tile bit k >= 2 = site lc_gb[k]: nibble 1 =
-// j-2 .. j+1 (the cone of r <= 1), nibble 2 = j+2, j+3, j-4, j-3 (with nibble
-// 1, r <= 3), nibble 0 = the columns and the two outer sites.  Program (the
-// nibble in registers; the host checks every layer's sites against it):
-//   r=5: 2 1 0 | D5 | r=4: 0 2 1 | D4 | r=3: 1 2 | D3 | r=2: 2 1 | D2 |
-//   r=1: 1 | D1 | r=0: 1 | probe (j = tile bit 6 = register bit 2)
-// — six re-layouts through the 32 KiB half-tile buffer for five passes (the
-// 8-site pass: five for four), three workgroups per CU.  D5 is two lookups
-// in the split radius-5 tables.  Global indices fit 32 bits (L_eff <= 32).
-// MASK: the layers' kick mask when known at compile time (0: read A.lc_mask).
-// The chains of the C2 sweep (two site groups split at j+2, the first merged
-// pass on j's group) all have kLcwMaskJ2 (lc_merge_wide): its instantiation
-// runs exactly the 32 kicked sites with no per-site branches, so the compiler
-// keeps the butterflies' results in renamed registers instead of copying them
-// back for the branch merges.
-static constexpr uint64_t kLcwMaskJ2 =
-    // l = 0: tile bits 2, 4..7, 10, 11 (sites j-5, j-2..j+1, j-4, j-3)
-    (0x33Dull) |
-    // l = 1: tile bits 3..11 (j+4, j-2..j+3, j-4, j-3)
-    (0x3FEull << 10) |
-    // l = 2: tile bits 4..9, 11 (j-2..j+3, j-3)
-    (0x2FCull << 20) |
-    // l = 3: tile bits 4..8 (j-2..j+2)
-    (0x07Cull << 30) |
-    // l = 4: tile bits 5..7 (j-1..j+1)
-    (0x038ull << 40) |
-    // l = 5: tile bit 6 (j)
-    (0x010ull << 50);
-
-template <int KIND, uint64_t MASK = 0>
-__global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
-  static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
-  __shared__ double s_half[kTile];
-  __shared__ double2 s_cone[kLcTab];
-  __shared__ double s_red[kThreads / 64][2];
-  const int t = threadIdx.x;
-  const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
-  const int og = A.octet_bits;
-  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
-  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
-  if (og && b >= A.batch) return;
-  const int inst = (int)((A.batch_start + b) / A.n_traj);
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcwMask + kLcwLayers) {  // the records: lanes 0 .. 19
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
-  constexpr int kConePerThread = (kLcTab + kThreads - 1) / kThreads;
-  double2 cv[kConePerThread];
-  const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
-#pragma unroll
-  for (int j = 0; j < kConePerThread; ++j) {
-    const int i = t + j * kThreads;
-    if (i < kLcTab) cv[j] = ct[i];
-  }
-  // tile bit -> global bit (wave-uniform), the window, the tile's base: the
-  // tile id's bits deposited, in order, into the global bits off the window
-  uint32_t gbit[kTileBits];
-  uint32_t win = 0;
-#pragma unroll
-  for (int k = 0; k < kTileBits; ++k) {
-    gbit[k] = 1u << A.lc_gb[k];
-    win |= gbit[k];
-  }
-  uint32_t tbase = 0;
-  {
-    uint32_t rest = (uint32_t)tile;
-    for (int g = 0; g < A.L_eff; ++g) {
-      if ((win >> g) & 1u) continue;
-      tbase |= (rest & 1u) << g;
-      rest >>= 1;
-    }
-  }
-  // the thread's part of the global index in layout LAY (register bits zero)
-  auto lane_part = [&](auto lay_tag) -> uint32_t {
-    constexpr int LAY = decltype(lay_tag)::value;
-    const int y = ybase<LAY>(t);
-    uint32_t x = 0;
-#pragma unroll
-    for (int k = 0; k < kTileBits; ++k)
-      if (k < 4 * LAY || k >= 4 * LAY + 4) x |= ((y >> k) & 1) ? gbit[k] : 0u;
-    return x;
-  };
-  using L0 = std::integral_constant<int, 0>;
-  using L1 = std::integral_constant<int, 1>;
-  using L2 = std::integral_constant<int, 2>;
-  // register r's part in layout LAY (uniform)
-  auto reg_part = [&](auto lay_tag, int r) -> uint32_t {
-    constexpr int LAY = decltype(lay_tag)::value;
-    return ((r & 1) ? gbit[4 * LAY] : 0u) | ((r & 2) ? gbit[4 * LAY + 1] : 0u) |
-           ((r & 4) ? gbit[4 * LAY + 2] : 0u) | ((r & 8) ? gbit[4 * LAY + 3] : 0u);
-  };
-  // the tile in layout 2 (threads = tile bits 0 .. 7: the columns in lane bits 0, 1)
-  double2 v[kRegs];
-  {
-    const int64_t vofs = octet_spread((int64_t)lane_part(L2{}), og) << 4;
-    const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      const char* a = src + (octet_spread((int64_t)(tbase | reg_part(L2{}, r)), og) << 4) + vofs;
-      const d2v w = __builtin_nontemporal_load((const d2v*)a);
-      v[r] = make_double2(w.x, w.y);
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0x4F70);  // records and tables landed, the tile's 16 loads in flight
-  const double cs = A.diag_conj ? -1.0 : 1.0;
-#pragma unroll
-  for (int j = 0; j < kConePerThread; ++j) {
-    const int i = t + j * kThreads;
-    if (i < kLcTab) s_cone[i] = make_double2(cv[j].x, cs * cv[j].y);
-  }
-  // (visible after the first re-layout's barrier)
-  const int jp = A.probe;
-  const int Lr = A.L_real;
-
-  // kicks of layer l on the kicked sites of nibble N (in registers)
-  auto kick = [&](auto n_tag, auto l_tag) {
-    constexpr int N = decltype(n_tag)::value;
-    constexpr int l = decltype(l_tag)::value;
-    if constexpr (MASK != 0) {
-      constexpr uint32_t m = (uint32_t)(MASK >> (10 * l));
-      if constexpr (4 * N + 0 >= 2 && ((m >> (4 * N + 0 - 2)) & 1u))
-        layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
-      if constexpr (4 * N + 1 >= 2 && ((m >> (4 * N + 1 - 2)) & 1u))
-        layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
-      if constexpr ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
-      if constexpr ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
-    } else {
-      const uint32_t m = (uint32_t)(A.lc_mask >> (10 * l));
-      if constexpr (4 * N + 0 >= 2)
-        if ((m >> (4 * N + 0 - 2)) & 1u) layer_f<KIND, 0, 0>(v, R.d(0, 12 * l + 4 * N + 0));
-      if constexpr (4 * N + 1 >= 2)
-        if ((m >> (4 * N + 1 - 2)) & 1u) layer_f<KIND, 0, 1>(v, R.d(0, 12 * l + 4 * N + 1));
-      if ((m >> (4 * N + 2 - 2)) & 1u) layer_f<KIND, 0, 2>(v, R.d(0, 12 * l + 4 * N + 2));
-      if ((m >> (4 * N + 3 - 2)) & 1u) layer_f<KIND, 0, 3>(v, R.d(0, 12 * l + 4 * N + 3));
-    }
-  };
-  // one cone-table factor in layout LAY: tab[((x ^ m) >> lo) & msk] per amplitude
-  // sw: the table's storage swizzle (0 none, 4 lc_pos4, 5 lc_pos5a), applied to
-  // the thread's base and the register offsets once (linear)
-  auto diag_tab = [&](auto lay_tag, uint32_t xm, int lo, int hi, const double2* tab, auto sw_tag) {
-    constexpr int LAY = decltype(lay_tag)::value;
-    constexpr int SW = decltype(sw_tag)::value;
-    auto pos = [](int i) { return SW == 4 ? lc_pos4(i) : (SW == 5 ? lc_pos5a(i) : i); };
-    const uint32_t msk = (1u << (hi - lo + 1)) - 1u;
-    const int base = pos((int)((xm >> lo) & msk));
-    const int o0 = pos((int)((gbit[4 * LAY] >> lo) & msk)), o1 = pos((int)((gbit[4 * LAY + 1] >> lo) & msk));
-    const int o2 = pos((int)((gbit[4 * LAY + 2] >> lo) & msk)), o3 = pos((int)((gbit[4 * LAY + 3] >> lo) & msk));
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-      const int off = ((r & 1) ? o0 : 0) ^ ((r & 2) ? o1 : 0) ^ ((r & 4) ? o2 : 0) ^ ((r & 8) ? o3 : 0);
-      v[r] = cmul(v[r], tab[base ^ off]);
-    }
-  };
-  // the cone diagonal after layer l (r = 5 - l), frame X mask m_l
-  auto diag = [&](auto lay_tag, auto l_tag) {
-    constexpr int l = decltype(l_tag)::value;
-    constexpr int rad = kLcwLayers - 1 - l;
-    const uint32_t xm = (tbase | lane_part(lay_tag)) ^ (uint32_t)R.bits(kLcwMask + l);
-    using S0 = std::integral_constant<int, 0>;
-    if constexpr (rad == 5) {
-      diag_tab(lay_tag, xm, max(0, jp - 5), jp, s_cone + kLcTab5a, std::integral_constant<int, 5>{});
-      diag_tab(lay_tag, xm, jp, min(Lr - 1, jp + 5), s_cone + kLcTab5b, S0{});
-    } else if constexpr (rad == 4) {
-      diag_tab(lay_tag, xm, max(0, jp - 4), min(Lr - 1, jp + 4), s_cone + lc_tab_off(4),
-               std::integral_constant<int, 4>{});
-    } else {
-      diag_tab(lay_tag, xm, max(0, jp - rad), min(Lr - 1, jp + rad), s_cone + lc_tab_off(rad), S0{});
-    }
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using C2 = std::integral_constant<int, 2>;
-  using C3 = std::integral_constant<int, 3>;
-  using C4 = std::integral_constant<int, 4>;
-  using C5 = std::integral_constant<int, 5>;
-  // r = 5: nibbles 2, 1, 0
-  kick(L2{}, C0{});
-  exchange_split<2, 1>(v, s_half, t);
-  kick(L1{}, C0{});
-  exchange_split<1, 0>(v, s_half, t);
-  kick(L0{}, C0{});
-  diag(L0{}, C0{});
-  // r = 4: nibbles 0, 2, 1
-  kick(L0{}, C1{});
-  exchange_split<0, 2>(v, s_half, t);
-  kick(L2{}, C1{});
-  exchange_split<2, 1>(v, s_half, t);
-  kick(L1{}, C1{});
-  diag(L1{}, C1{});
-  // r = 3: nibbles 1, 2
-  kick(L1{}, C2{});
-  exchange_split<1, 2>(v, s_half, t);
-  kick(L2{}, C2{});
-  diag(L2{}, C2{});
-  // r = 2: nibbles 2, 1
-  kick(L2{}, C3{});
-  exchange_split<2, 1>(v, s_half, t);
-  kick(L1{}, C3{});
-  diag(L1{}, C3{});
-  // r = 1, r = 0: nibble 1
-  kick(L1{}, C4{});
-  diag(L1{}, C4{});
-  kick(L1{}, C5{});
-  // probe: j at register bit 2 of layout 1; the frame's final X on j flips it
-  double ptot = 0.0, pz = 0.0;
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) {
-    const double p2 = fma(v[r].x, v[r].x, v[r].y * v[r].y);
-    ptot += p2;
-    pz += ((r >> 2) & 1) ? -p2 : p2;
-  }
-  if ((R.bits(kLcwMask + kLcwLayers - 1) >> jp) & 1) pz = -pz;
-  const double g2 = R.d(0, kLcwG2);
-  const int wave = t >> 6, lane = t & 63;
-  const double tot = wave_sum(ptot) * g2;
-  const double z = wave_sum(pz) * g2;
-  if (lane == 0) {
-    s_red[wave][0] = tot;
-    s_red[wave][1] = z;
-  }
-  __syncthreads();
-  if (t < 2) {
-    double acc = 0.0;
-    for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
-    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
-  }
-}
-
 template <int NIBS, int KIND, int MC>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
@@ -1929,7 +1115,8 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, int mc
   }
 }
 
-hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream) {
+hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream,
+                       int* lc_variant) {
   if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch || batch > 65535 ||
       a.n_chunks > kMaxChunks)
     return hipErrorInvalidValue;
@@ -1938,57 +1125,7 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
     return hipErrorInvalidValue;
   // octet layout: the eight states of an octet on consecutive blocks
   dim3 grid = a.octet_bits ? dim3(n_tiles * 8, (batch + 7) / 8) : dim3(n_tiles, batch);
-  if (shape == kShapeLC && a.lc_wide) {
-    // 10-site light-cone pass: six layers, tile bits 0, 1 = global 0, 1, the
-    // probe at tile bit 6, twelve distinct global bits inside the state
-    if (a.meas != kMeasProbe || !a.no_store || a.lc_layers != kLcwLayers || a.n_obs < 2 ||
-        !a.lc_diag || a.lc_gb[0] != 0 || a.lc_gb[1] != 1 || a.lc_gb[6] != a.probe ||
-        (kind != kKindRX && kind != kKindRY))
-      return hipErrorInvalidValue;
-    uint64_t seen = 0;
-    for (int k = 0; k < kTileBits; ++k) {
-      if (a.lc_gb[k] < 0 || a.lc_gb[k] >= a.L_eff || ((seen >> a.lc_gb[k]) & 1)) return hipErrorInvalidValue;
-      seen |= 1ull << a.lc_gb[k];
-    }
-    if (a.lc_mask == kLcwMaskJ2)
-      hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX, kLcwMaskJ2>
-                                          : dtc_lcw_final<kKindRY, kLcwMaskJ2>),
-                         grid, dim3(kThreads), 0, stream, a);
-    else
-      hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw_final<kKindRX> : dtc_lcw_final<kKindRY>), grid,
-                         dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
-  }
-  if (shape == kShapeLC) {
-    // measure-only light-cone pass: probe, window at tile bits 4..11 (c = 4)
-    if (a.c != 4 || a.act != 0xFF0 || a.meas != kMeasProbe || !a.no_store || a.lc_layers < 1 ||
-        a.lc_layers > kLcLayers || a.n_obs < 2 || !a.lc_diag)
-      return hipErrorInvalidValue;
-    // several tiles per workgroup (register double buffer) when they divide the state
-    // default: one tile per workgroup, re-layouts through half the LDS, three
-    // workgroups per CU (r2ar: 6.15 -> 5.42 ms); lc_split = 0 keeps the
-    // 64 KiB exchange with lc_tpb tiles per workgroup (development A/B:
-    // DTC_LC_SPLIT / DTC_LC_TPB, read once by dtc_open)
-    int tpb = a.lc_tpb > 0 ? a.lc_tpb : kLcTilesPerGroup;
-    if (a.lc_split) {
-      if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((kind == kKindRX ? dtc_lc_final_split<kKindRX> : dtc_lc_final_split<kKindRY>),
-                         grid, dim3(kThreads), 0, stream, a);
-      return hipGetLastError();
-    }
-    while (tpb > 1 && n_tiles % tpb) tpb >>= 1;
-    if (tpb != 1 && tpb != 2 && tpb != 4) tpb = 1;
-    grid.x = (a.octet_bits ? 8 : 1) * n_tiles / tpb;
-    if (kind != kKindRX && kind != kKindRY) return hipErrorInvalidValue;
-    const bool rx = kind == kKindRX;
-    if (tpb == 4)
-      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 4> : dtc_lc_final<kKindRY, 4>), grid, dim3(kThreads), 0, stream, a);
-    else if (tpb == 2)
-      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 2> : dtc_lc_final<kKindRY, 2>), grid, dim3(kThreads), 0, stream, a);
-    else
-      hipLaunchKernelGGL((rx ? dtc_lc_final<kKindRX, 1> : dtc_lc_final<kKindRY, 1>), grid, dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
-  }
+  if (shape == kShapeLC) return launch_lightcone(a, grid, kind, stream, lc_variant);
   int nibs = 0;
   for (int n = 0; n < 3; ++n)
     if (a.act & (0xF << (4 * n))) nibs |= 1 << n;
@@ -2091,6 +1228,125 @@ hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* id
 // (c, r), r < c.  blockIdx.y = pair; each thread moves kSwapPerThread
 // amplitudes of both pieces, 16-B accesses 256 threads apart (1 KiB per wave
 // instruction, coalesced), streaming hints (every byte is touched once).
+// The last pre-exchange kick pass of one slice fused with the virtual ranks'
+// in-place all-to-all of that slice (dtc_shard_kick_exchange_slice; C5 on one
+// GPU, sharded.py inplace): the slice of piece (shard r, chunk c) is a
+// 2^L_eff-amplitude state, pieces state_len apart, b = r W + c.  A workgroup
+// takes tile i of the pair (r, c), (c, r) -- both tiles loaded before either
+// is stored -- kicks each and stores it at its partner's place (the diagonal
+// pieces in place): the exchange costs no pass of its own (it was 32 B per
+// amplitude of the off-diagonal pieces, 76 of 473 ms per L=34 period, r3zk).
+// grid = (tiles, W (W + 1) / 2 pair slots); contiguous states (octet_bits 0).
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kick_swap_pass(PassArgs A, int k_bits) {
+  static_assert(KIND == kKindRX || KIND == kKindRY || KIND == kKindGen, "unitary kick kinds");
+  using RP = RoundPlan<NIBS, kShapeK>;
+  __shared__ double2 s_tile[kTile];
+  const int t = threadIdx.x;
+  const int W = 1 << k_bits;
+  int q = blockIdx.y, r = 0;
+  while (q >= W - r) {  // pair slot -> (r, c), r <= c
+    q -= W - r;
+    ++r;
+  }
+  const int c_ch = r + q;
+  const int64_t b1 = (int64_t)r * W + c_ch, b2 = (int64_t)c_ch * W + r;
+  const int64_t tile = blockIdx.x;
+  RecRegs R;  // every piece is the same trajectory: piece b1's records
+  {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs + b1 * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < 8 * kRecPerState) {
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
+  const int c = A.c, s = A.s;
+  const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
+  TileMap M;
+  M.c = c;
+  M.s = s;
+  M.cmask = (1 << c) - 1;
+  M.tbase = ((tile & mid_mask) << c) | ((tile >> A.tile_bits_mid) << (s + kTileBits - c));
+  const int64_t vofs = M.rel(ybase<RP::IO>(t)) << 4;
+  auto tile_ofs = [&](int rr) -> int64_t { return (M.tbase | M.rel(rr << (4 * RP::IO))) << 4; };
+  const char* p1 = (const char*)(A.src + b1 * A.state_len);
+  const char* p2 = (const char*)(A.src + b2 * A.state_len);
+  double2 v[kRegs], w[kRegs];
+#pragma unroll
+  for (int rr = 0; rr < kRegs; ++rr) {
+    const d2v x = __builtin_nontemporal_load((const d2v*)(p1 + tile_ofs(rr) + vofs));
+    v[rr] = make_double2(x.x, x.y);
+  }
+  if (b2 != b1) {
+#pragma unroll
+    for (int rr = 0; rr < kRegs; ++rr) {
+      const d2v x = __builtin_nontemporal_load((const d2v*)(p2 + tile_ofs(rr) + vofs));
+      w[rr] = make_double2(x.x, x.y);
+    }
+  }
+  const double2 gph = make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1));
+  // the kick-only pass of pass_body: rounds IO -> 0 -> O, the global factor,
+  // back to the IO layout
+  auto kick = [&](double2 (&u)[kRegs]) {
+    if constexpr (RP::nIO) apply_nibble<RP::IO, KIND>(u, R, 0);
+    if constexpr (RP::n0) {
+      exchange<RP::IO, 0>(u, s_tile, t);
+      apply_nibble<0, KIND>(u, R, 0);
+    }
+    if constexpr (RP::nO) {
+      exchange<RP::n0 ? 0 : RP::IO, RP::O>(u, s_tile, t);
+      apply_nibble<RP::O, KIND>(u, R, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < kRegs; ++rr) u[rr] = cmul(u[rr], gph);
+    exchange<RP::d_lay, RP::IO>(u, s_tile, t);
+  };
+  auto store = [&](const double2 (&u)[kRegs], const char* base) {
+    char* p = (char*)base;
+#pragma unroll
+    for (int rr = 0; rr < kRegs; ++rr) {
+      d2v x = {u[rr].x, u[rr].y};
+      __builtin_nontemporal_store(x, (d2v*)(p + tile_ofs(rr) + vofs));
+    }
+  };
+  kick(v);
+  store(v, p2);  // (r, c) -> (c, r); the diagonal piece in place
+  if (b2 != b1) {
+    kick(w);
+    store(w, p1);
+  }
+}
+
+hipError_t launch_kick_swap(const PassArgs& a, int k_bits, int kind, hipStream_t stream) {
+  const int W = 1 << k_bits;
+  if (k_bits < 1 || k_bits > 6 || a.batch != W * W || a.octet_bits != 0 || a.src != a.dst ||
+      a.L_eff < kTileBits || a.L_eff > 32 || a.n_chunks > kMaxChunks)
+    return hipErrorInvalidValue;
+  int nibs = 0;
+  for (int n = 0; n < 3; ++n)
+    if (a.act & (0xF << (4 * n))) nibs |= 1 << n;
+  const dim3 grid(1u << (a.L_eff - kTileBits), (unsigned)(W * (W + 1) / 2)), block(kThreads);
+  auto go = [&](auto nibs_tag) -> hipError_t {
+    constexpr int N = decltype(nibs_tag)::value;
+    switch (kind) {
+      case kKindRX: hipLaunchKernelGGL((dtc_kick_swap_pass<N, kKindRX>), grid, block, 0, stream, a, k_bits); break;
+      case kKindRY: hipLaunchKernelGGL((dtc_kick_swap_pass<N, kKindRY>), grid, block, 0, stream, a, k_bits); break;
+      case kKindGen: hipLaunchKernelGGL((dtc_kick_swap_pass<N, kKindGen>), grid, block, 0, stream, a, k_bits); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  };
+  switch (nibs) {
+    case 4: return go(std::integral_constant<int, 4>{});
+    case 6: return go(std::integral_constant<int, 6>{});
+    case 7: return go(std::integral_constant<int, 7>{});
+    default: return hipErrorInvalidValue;
+  }
+}
+
 static constexpr int kSwapPerThread = 4;
 
 __global__ __launch_bounds__(256) void exchange_swap_kernel(double2* __restrict__ state, int nl,

@@ -349,6 +349,20 @@ class DtcEngine:
             self._ctx, ctypes.byref(shard), ctypes.c_int32(slice_bits), ctypes.c_int32(slice_),
             ctypes.c_void_p(state_ptr)))
 
+    def shard_kick_exchange_slice(self, spec: SweepSpec, shard, period: int, pre_mask: int,
+                                  slice_bits: int, slice_: int, state_ptr: int,
+                                  seed: int = 0x5EED0001, traj: int = 0):
+        """Virtual ranks: ``shard_kick_slice`` (chunk bits = n_global) and
+        ``shard_exchange_slice`` of slice ``slice_`` as one step -- the last
+        site group's kick pass stores each piece at its partner's place
+        (dtc_shard_kick_exchange_slice), so the exchange moves no bytes of its
+        own."""
+        _capi.check(self._lib.dtc_shard_kick_exchange_slice(
+            self._ctx, ctypes.byref(self._problem(spec)), ctypes.byref(self._noise(spec)),
+            ctypes.byref(shard), ctypes.c_uint64(seed), ctypes.c_int64(traj),
+            ctypes.c_int32(period), ctypes.c_uint64(pre_mask), ctypes.c_int32(slice_bits),
+            ctypes.c_int32(slice_), ctypes.c_void_p(state_ptr)))
+
     def stream_handle(self) -> int:
         """The engine's hipStream_t (for torch.cuda.ExternalStream)."""
         h = ctypes.c_void_p()
@@ -375,6 +389,13 @@ class DtcEngine:
                                                    ctypes.byref(ms), ctypes.byref(by)))
             out[k] = {"launches": n.value, "total_ms": ms.value, "bytes": by.value}
         return out
+
+    def lightcone_counts(self):
+        """Light-cone ends launched since the engine opened, by kernel
+        (dtc_lightcone_counts): 8-site window, 10-site generic, 10-site C2 form."""
+        c = (ctypes.c_int64 * 3)()
+        _capi.check(self._lib.dtc_lightcone_counts(self._ctx, c))
+        return {"lc8": c[0], "lcw": c[1], "lcw2": c[2]}
 
     def device_info(self):
         name = ctypes.create_string_buffer(256)

@@ -194,6 +194,10 @@ class EngineStepper:
     def exchange_slice(self, layout: ShardLayout, slice_bits, slice_, buf):
         self.engine.shard_exchange_slice(layout.to_c(), slice_bits, slice_, buf.data_ptr())
 
+    def kick_exchange_slice(self, spec, layout, seed, traj, period, pre, slice_bits, slice_, buf):
+        self.engine.shard_kick_exchange_slice(spec, layout.to_c(), period, pre, slice_bits, slice_,
+                                              buf.data_ptr(), seed, traj)
+
     def set_basis(self, spec, layout, seed, traj, buf):
         import torch
 
@@ -287,6 +291,101 @@ def slice_p2p_plan(rank: int, W: int):
     return ops
 
 
+class LoopbackHub:
+    """In-process point-to-point transport between virtual ranks with RCCL's
+    stream semantics, so the real-rank branch of ``_SliceExchange`` (side
+    stream, ``batch_isend_irecv``, ``Work.wait``) runs on one GPU, where RCCL
+    itself refuses two ranks (profiles/r3w_rccl_same_gpu_probe.txt).
+
+    Each rank has its own transport stream (RCCL's internal stream).  At issue
+    an isend / irecv records an event on the stream that is current then (the
+    caller's side stream), as RCCL makes its stream wait on the current one.
+    A send from r to d is matched with d's receive from r in posting order;
+    the pair becomes one device copy on the sender's transport stream after
+    both events, and both Works complete with it: ``Work.wait()`` makes the
+    current stream wait for that copy (RCCL's ``Work.wait``).  Waiting on an
+    unmatched op raises (with RCCL it would spin until the peer posts).
+    ``log`` records (rank, kind, peer) per op for the op-list check."""
+
+    def __init__(self, world: int):
+        import torch
+
+        self.world = world
+        self.streams = [torch.cuda.Stream() for _ in range(world)]
+        self.pending = {}  # (src, dst) -> list of ("send" | "recv", tensor, event, work)
+        self.log = []
+
+    def group(self, rank: int) -> "LoopbackGroup":
+        return LoopbackGroup(self, rank)
+
+    def _post(self, kind, rank, peer, tensor):
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        work = _LoopbackWork()
+        key = (rank, peer) if kind == "isend" else (peer, rank)
+        q = self.pending.setdefault(key, [])
+        self.log.append((rank, kind, peer))
+        side = "send" if kind == "isend" else "recv"
+        other = next((i for i, e in enumerate(q) if e[0] != side), None)
+        if other is None:
+            q.append((side, tensor, ev, work))
+            return work
+        o_side, o_tensor, o_ev, o_work = q.pop(other)
+        snd, rcv = (tensor, o_tensor) if side == "send" else (o_tensor, tensor)
+        src_rank = key[0]
+        st = self.streams[src_rank]
+        st.wait_event(ev)
+        st.wait_event(o_ev)
+        if snd.shape != rcv.shape:
+            raise RuntimeError(f"loopback: send {tuple(snd.shape)} != recv {tuple(rcv.shape)}")
+        with torch.cuda.stream(st):
+            rcv.copy_(snd)
+            done = torch.cuda.Event()
+            done.record(st)
+        work.done = o_work.done = done
+        return work
+
+
+class _LoopbackWork:
+    done = None
+
+    def wait(self):
+        import torch
+
+        if self.done is None:
+            raise RuntimeError("loopback: wait() on an op its peer has not posted")
+        torch.cuda.current_stream().wait_event(self.done)
+
+
+class LoopbackGroup:
+    """One virtual rank's view of a LoopbackHub, with the torch.distributed
+    point-to-point surface ``_SliceExchange`` uses (``P2POp``, ``isend``,
+    ``irecv``, ``batch_isend_irecv``)."""
+
+    def __init__(self, hub: LoopbackHub, rank: int):
+        self.hub, self.rank = hub, rank
+
+    # module-like surface (the group passed as the ops' group is this object)
+    def isend(self):  # marker, as torch.distributed.isend in P2POp
+        raise NotImplementedError
+
+    def irecv(self):
+        raise NotImplementedError
+
+    class P2POp:
+        def __init__(self, op, tensor, peer, group):
+            self.op, self.tensor, self.peer, self.group = op, tensor, peer, group
+
+    def batch_isend_irecv(self, ops):
+        works = []
+        for o in ops:
+            kind = "isend" if o.op == o.group.isend else "irecv"
+            works.append(self.hub._post(kind, self.rank, o.peer, o.tensor))
+        return works
+
+
 class _SliceExchange:
     """All-to-all of one period as S slice transfers, each started as soon as
     its slice has been kicked.
@@ -315,6 +414,14 @@ class _SliceExchange:
         self.cuda = hasattr(stepper, "stream")
         self.eng = stepper.stream() if self.cuda else None
         self.side = torch.cuda.Stream() if (self.cuda and not inplace) else None
+        # the point-to-point layer: torch.distributed (RCCL / gloo), or a
+        # virtual rank's LoopbackGroup (same surface, one process)
+        if isinstance(group, LoopbackGroup):
+            self.comm = group
+        else:
+            import torch.distributed as dist
+
+            self.comm = dist
         self.works = []
         self.t_events = []  # (start, end) per period, side stream (engine stream in place)
 
@@ -328,7 +435,6 @@ class _SliceExchange:
 
     def send(self, s, src, dst, layout=None):
         import torch
-        import torch.distributed as dist
 
         W, S = self.W, self.S
         if self.inplace:
@@ -355,20 +461,28 @@ class _SliceExchange:
             sv, dv = src.view(W, S, -1), dst.view(W, S, -1)
             r = self.rank
             dv[r, s].copy_(sv[r, s])
+            comm = self.comm
             ops = []
             for kind, peer, chunk in slice_p2p_plan(r, W):
                 if kind == "isend":
-                    ops.append(dist.P2POp(dist.isend, torch.view_as_real(sv[chunk, s]), peer,
+                    ops.append(comm.P2POp(comm.isend, torch.view_as_real(sv[chunk, s]), peer,
                                           self.group))
                 else:
-                    ops.append(dist.P2POp(dist.irecv, torch.view_as_real(dv[chunk, s]), peer,
+                    ops.append(comm.P2POp(comm.irecv, torch.view_as_real(dv[chunk, s]), peer,
                                           self.group))
-            reqs = dist.batch_isend_irecv(ops)
+            reqs = comm.batch_isend_irecv(ops)
             if self.cuda:
                 self.works.extend(reqs)
             else:
                 for q in reqs:
                     q.wait()
+
+    def kick_and_swap(self, s, fn):
+        """In place: ``fn`` kicks slice s and exchanges it in one step (the
+        fused kick+exchange pass, ordered on the engine stream)."""
+        if self.cuda:
+            self._mark_start(s, self.eng)
+        fn()
 
     def finish(self):
         import torch
@@ -398,7 +512,7 @@ class _SliceExchange:
 def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0,
                               traj: int = 0, seed: int = 0x5EED0001, rank: int = 0,
                               world: int = 1, group=None, buffers=None, stats=None,
-                              inplace: bool = False):
+                              inplace: bool = False, fuse_kick_exchange: bool = True):
     """``sharded_forward`` with the exchange overlapped and no host round trip
     per period (the C5 schedule on the GPU node).
 
@@ -423,6 +537,70 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     ``stats`` (dict, optional) receives the per-period exchange windows (ms,
     side-stream events; engine-stream events in place) and the per-period wall
     of the engine stream (``period_ms``) on the GPU."""
+    return _run_rank(_pipelined_rank(stepper, spec, n_global, inst=inst, traj=traj, seed=seed,
+                                     rank=rank, world=world, group=group, buffers=buffers,
+                                     stats=stats, inplace=inplace,
+                                     fuse_kick_exchange=fuse_kick_exchange), group)
+
+
+def _run_rank(gen, group):
+    """Drive one rank's generator in its own process: exchange marks are
+    no-ops, the join is the process group's all-reduce."""
+    reply = None
+    while True:
+        try:
+            kind, val = gen.send(reply)
+        except StopIteration as e:
+            return e.value
+        reply = _allreduce(val, group) if kind == "allreduce" else None
+
+
+def loopback_forward_pipelined(steppers, spec: SweepSpec, n_global: int, *, inst: int = 0,
+                               traj: int = 0, seed: int = 0x5EED0001):
+    """The real-rank C5 pipeline of 2^n_global ranks in one process on one
+    GPU: rank r = ``steppers[r]`` (its own engine context and stream, its own
+    two shard buffers), ``_SliceExchange`` in its world-W branch over a
+    LoopbackHub (RCCL's stream semantics, device copies).  The ranks advance
+    in lock step between the yields of ``_pipelined_rank``; the join sums their
+    vectors.  Returns (rank 0's result, the hub's op log)."""
+    W = 1 << n_global
+    if len(steppers) != W:
+        raise ValueError("one stepper per rank")
+    hub = LoopbackHub(W)
+    gens = [_pipelined_rank(steppers[r], spec, n_global, inst=inst, traj=traj, seed=seed, rank=r,
+                            world=W, group=hub.group(r)) for r in range(W)]
+    replies = [None] * W
+    results = [None] * W
+    while True:
+        msgs = {}
+        for r in range(W):
+            try:
+                msgs[r] = gens[r].send(replies[r])
+            except StopIteration as e:
+                results[r] = e.value
+        if not msgs:
+            break
+        kinds = {m[0] for m in msgs.values()}
+        if len(msgs) != W or len(kinds) != 1:
+            raise RuntimeError(f"loopback ranks out of step: {sorted(msgs)} {kinds}")
+        if kinds == {"allreduce"}:
+            total = sum(m[1] for m in msgs.values())
+            replies = [np.array(total) for _ in range(W)]
+        else:
+            replies = [None] * W
+    return results[0], hub.log
+
+
+def _pipelined_rank(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0, traj: int = 0,
+                    seed: int = 0x5EED0001, rank: int = 0, world: int = 1, group=None,
+                    buffers=None, stats=None, inplace: bool = False,
+                    fuse_kick_exchange: bool = True):
+    """One rank's ``sharded_forward_pipelined`` as a generator: it yields
+    ("exchange", None) once a period's slice transfers are all posted (before
+    waiting for them) and ("allreduce", vec) for the final join, receiving the
+    sum.  ``_run_rank`` drives one process's rank (the yields are no-ops, the
+    join is RCCL / gloo); ``loopback_forward_pipelined`` drives all the virtual
+    ranks of one GPU in lock step over a LoopbackHub."""
     import torch
 
     L, T = spec.L, spec.T
@@ -458,6 +636,7 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     if inplace and not chunked:
         raise ValueError("the in-place exchange needs chunks of at least one tile")
     P = T - 1 + spec.t_offset
+    fuse_kick = fuse_kick_exchange and hasattr(stepper, "kick_exchange_slice")
     obs = stepper.obs_buffer(P + 1, n_sh, 1 + nl)
     layouts = [lay]
     xch = _SliceExchange(stepper, W, S, rank, world, group, inplace=inplace,
@@ -483,10 +662,17 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
             stepper.step_async(spec, lay, seed, traj, inst, p, whole, False, 0, A, A, None)
             pre &= ~whole
         for sl in range(S):
+            if inplace and pre and fuse_kick:
+                # one GPU: the slice's last kick pass stores each piece at its
+                # partner's place (the exchange costs no pass of its own)
+                xch.kick_and_swap(sl, lambda: stepper.kick_exchange_slice(
+                    spec, lay, seed, traj, p, pre, slice_bits, sl, A))
+                continue
             if pre:
                 stepper.kick_slice(spec, lay, seed, traj, p, pre, n_global, slice_bits if chunked
                                    else 0, sl, A)
             xch.send(sl, A, Bf, lay)
+        yield ("exchange", None)  # every rank's transfers of the period are posted
         xch.finish()
         lay = lay.exchanged()
         post = post_bits if p < P else 0
@@ -497,7 +683,7 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     stepper.synchronize()
     o = obs.cpu().numpy() if hasattr(obs, "cpu") else np.asarray(obs)
     z = np.stack([z_from_obs(layouts[p], o[p]) for p in range(P + 1)])
-    z = _allreduce(z, group)
+    z = yield ("allreduce", z)
     zinit = 1.0 if z[0, 1 + spec.probe_site] >= 0 else -1.0
     zs = np.zeros((T, L))
     norm = np.zeros(T)

@@ -252,6 +252,34 @@ def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe,
         assert (n_wide < n_narrow) == wide, (n_wide, n_narrow)
 
 
+@pytest.mark.parametrize("L,pol,state,toff,g,p", [
+    (20, "x", "vacuum", 0, 0.97, 0.05),   # BASELINE configs[1]'s kicks and noise
+    (20, "y", "neel", 1, 0.93, 0.1),
+    (21, "x", "neel", 0, 0.91, 0.1),      # 12 + 9 sites: 128-B columns in the forward passes
+    (21, "y", "vacuum", 1, 0.97, 0.0),    # noiseless: identity frames
+])
+def test_lcw2_c2_form(pkg, monkeypatch, L, pol, state, toff, g, p):
+    """The C2 chains' 10-site light-cone end runs as dtc_lcw2_final (three LDS
+    re-layouts, row swaps, pre-masked cone tables): its launches are counted
+    (dtc_lightcone_counts) and its echo equals the C oracle per trajectory
+    (1e-10) and the 8-site form (DTC_NO_LCW) to 1e-12."""
+    rng = np.random.default_rng(L * 7 + toff)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=9, hs=hs, phis=phis, g=g, noise_prob=p, use_noise=int(p > 0),
+                         polarization=pol, initial_state=state, t_offset=toff)
+    with pkg.DtcEngine(0) as eng:
+        got = eng.autocorr(spec, 3, seed=91)
+        counts = eng.lightcone_counts()
+    assert counts["lcw2"] > 0 and counts["lcw"] == 0, counts
+    _cmp(got, c_oracle.autocorr(spec, 3, seed=91))
+    with monkeypatch.context() as m:
+        m.setenv("DTC_NO_LCW", "1")
+        with pkg.DtcEngine(0) as eng:
+            narrow = eng.autocorr(spec, 3, seed=91)
+            assert eng.lightcone_counts()["lcw2"] == 0
+    assert np.abs(got["echo"] - narrow["echo"]).max() < 1e-12
+
+
 def test_independent_t_matches_oracle(pkg, engine):
     """--independent_t: every t from its own trajectories (t_first runs of
     t + t_offset periods, fast.py:219-221) -- engine = C oracle per trajectory."""

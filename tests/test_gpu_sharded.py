@@ -131,6 +131,13 @@ def test_pipelined_inplace_virtual_shards_match_engine(pkg, engine, stepper, L, 
                               want_zsite=True)
         assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
         assert np.abs(got["norm"] - 1.0).max() < 1e-10
+        # the fused kick+exchange pass (dtc_shard_kick_exchange_slice, the
+        # default) against the kick pass followed by the swap kernel: the same
+        # kicks in another kernel (bit for bit for the factored kinds; the
+        # general 2x2 contracts its FMAs its own way: last-bit differences)
+        sep = pkg.sharded.sharded_forward_pipelined(stepper, spec, k, inst=1, traj=traj, seed=77,
+                                                    inplace=True, fuse_kick_exchange=False)
+        assert np.abs(got["zsite"] - sep["zsite"]).max() < 1e-13
 
 
 def test_exchange_slice_is_the_all_to_all(pkg, engine, stepper):
@@ -152,3 +159,46 @@ def test_exchange_slice_is_the_all_to_all(pkg, engine, stepper):
         stepper.exchange_slice(lay, 2, s, y)
     engine.synchronize()
     assert torch.equal(y, x)
+
+
+@pytest.mark.parametrize("L,k,T,p,state,pol,toff", [
+    (22, 3, 5, 0.05, "neel", "x", 0),
+    (26, 2, 4, 0.1, "vacuum", "circular_left", 1),
+    (30, 3, 4, 0.05, "vacuum", "x", 0),
+])
+def test_loopback_real_rank_exchange(pkg, engine, L, k, T, p, state, pol, toff):
+    """The C5 pipeline's real-rank branch on one GPU: 2^k ranks, each its own
+    engine context (stream) and two shard buffers, ``_SliceExchange`` with
+    world = 2^k -- side stream waiting on the engine stream, batch_isend_irecv
+    issued under the side stream, Work.wait() on it, the engine stream waiting
+    for it -- over LoopbackHub (RCCL's stream semantics; RCCL itself refuses
+    two ranks on one GPU).  Per-site <Z_i(t)> equal dtc_autocorr's to 1e-10 and
+    every rank posts exactly slice_p2p_plan's ops, slice after slice."""
+    import torch
+
+    rng = np.random.default_rng(L * 17 + k)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+    one = dataclasses.replace(spec, hs=hs[1:2], phis=phis[1:2])
+    W = 1 << k
+    engines = [pkg.DtcEngine(0) for _ in range(W)]
+    try:
+        steppers = [pkg.sharded.EngineStepper(e) for e in engines]
+        got, log = pkg.sharded.loopback_forward_pipelined(steppers, spec, k, inst=1, traj=3,
+                                                          seed=77)
+        del steppers
+    finally:
+        for e in engines:
+            e.close()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    ref = engine.autocorr(one, 1, seed=77, traj_offset=3, want_echo=False, want_zsite=True)
+    assert np.abs(got["zsite"] - ref["zsite"][0, 0]).max() < TOL
+    assert np.abs(got["fwd"] - ref["fwd"][0, 0]).max() < TOL
+    assert np.abs(got["norm"] - 1.0).max() < 1e-10
+    for r in range(W):
+        plan = [(kind, peer) for kind, peer, _ in pkg.sharded.slice_p2p_plan(r, W)]
+        ops = [(kind, peer) for rr, kind, peer in log if rr == r]
+        assert ops and len(ops) % len(plan) == 0
+        assert ops == plan * (len(ops) // len(plan)), r
