@@ -119,6 +119,7 @@ struct dtc_ctx {
   int prefix_octet = 0;      // layout the prefix states were built in
   int64_t st_n[DTC_KERNEL_KINDS] = {};
   int64_t lc_launches[3] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
+  bool dual = true;  // DTC_NO_DUAL: echo chains start with a pass of their own
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
   std::vector<Pending> pending;
@@ -541,7 +542,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
                      const PassSpec& ps, const double2* src, double2* dst, int meas_mode,
                      int meas_at_end, int n_obs, double* meas_out, int64_t meas_stride,
                      const dtc::KickRec* recs = nullptr, int meas_parts = 0,
-                     int no_store = 0, const int64_t* basis = nullptr, int swap_k = 0) {
+                     int no_store = 0, const int64_t* basis = nullptr, int swap_k = 0,
+                     const dtc::KickRec* recs2 = nullptr, double2* dst2 = nullptr) {
   const int shape = pass_shape(ps);
   if (shape < 0) return fail(DTC_EINVAL, "internal: empty pass");
   const int kind = pass_kind(rc, ps, shape);
@@ -628,6 +630,10 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   for (int k = 0; k < dtc::kTileBits; ++k) A.lc_gb[k] = ps.lc_gb[k];
   A.batch = batch;
   A.n_obs = n_obs;
+  A.recs2 = recs2;
+  A.dst2 = dst2;
+  if (dst2 && (!recs2 || shape != dtc::kShapeKDK || no_store || basis))
+    return fail(DTC_EINVAL, "internal: a dual pass is a stored K-D-K with its branch's records");
   const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
                               : (ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS);
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -650,7 +656,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     // algorithmic bytes: a read and a store per amplitude, or one of them
     // (measure-only passes store nothing, a basis-synthesising pass reads nothing)
-    const double per_amp = (no_store || basis) ? 16.0 : 32.0;
+    const double per_amp = (no_store || basis) ? 16.0 : (dst2 ? 48.0 : 32.0);
     ctx->pending.push_back(Pending{kernel, e0, e1, per_amp * (double)((int64_t)1 << A.L_eff) * batch});
   }
   if (meas_mode != dtc::kMeasNone && meas_out)
@@ -670,31 +676,49 @@ struct Launch {
   int64_t meas_stride;
   int no_store = 0;  // the pass's output is never read again (last pass of an echo chain)
   const int64_t* basis = nullptr;  // first pass of a sweep: src = the basis states (synthesised)
+  // dual pass (dtc_kdk_dual): ps is a forward K-D-K that also starts an echo
+  // chain -- ps2 = {ps's pre-kick, the echo's first kick layer as post}, its
+  // tile after the pre-kick, kicked by ps2's post, goes to dst2
+  double2* dst2 = nullptr;
+  PassSpec ps2{};
 };
 
 int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
                  const std::vector<Launch>& L) {
+  // one record row per launch, two for a dual pass (its echo branch's kicks)
+  std::vector<size_t> row0(L.size() + 1);
+  ctx->pk_host.clear();
+  for (size_t i = 0; i < L.size(); ++i) {
+    row0[i] = ctx->pk_host.size();
+    ctx->pk_host.push_back(pass_kick(rc, L[i].ps));
+    if (L[i].dst2) ctx->pk_host.push_back(pass_kick(rc, L[i].ps2));
+  }
+  row0[L.size()] = ctx->pk_host.size();
+  const size_t n_rows = ctx->pk_host.size();
   const size_t per_pass = (size_t)batch * dtc::kRecPerState * sizeof(dtc::KickRec);
-  const size_t seg = std::max<size_t>(1, std::min<size_t>(L.size(), (size_t)(256u << 20) / per_pass));
+  const size_t seg = std::max<size_t>(2, std::min<size_t>(n_rows, (size_t)(256u << 20) / per_pass));
   DTC_TRY(ensure(ctx->recs, seg * per_pass));
-  ctx->pk_host.resize(L.size());
-  for (size_t i = 0; i < L.size(); ++i) ctx->pk_host[i] = pass_kick(rc, L[i].ps);
-  DTC_TRY(ensure(ctx->pk, L.size() * sizeof(dtc::PassKick)));
-  DTC_HIP(hipMemcpyAsync(ctx->pk.p, ctx->pk_host.data(), L.size() * sizeof(dtc::PassKick),
+  DTC_TRY(ensure(ctx->pk, n_rows * sizeof(dtc::PassKick)));
+  DTC_HIP(hipMemcpyAsync(ctx->pk.p, ctx->pk_host.data(), n_rows * sizeof(dtc::PassKick),
                          hipMemcpyHostToDevice, ctx->stream));
-  for (size_t i0 = 0; i0 < L.size(); i0 += seg) {
-    const size_t n = std::min(seg, L.size() - i0);
+  // segments of whole launches whose rows fit the record buffer
+  for (size_t i0 = 0; i0 < L.size();) {
+    size_t i1 = i0;
+    while (i1 < L.size() && row0[i1 + 1] - row0[i0] <= seg) ++i1;
     dtc::PrepArgs P = prep_args(ctx, rc, batch_start, batch);
-    P.passes = (const dtc::PassKick*)ctx->pk.p + i0;
-    P.n_pass = (int)n;
+    P.passes = (const dtc::PassKick*)ctx->pk.p + row0[i0];
+    P.n_pass = (int)(row0[i1] - row0[i0]);
     P.out = (dtc::KickRec*)ctx->recs.p;
     DTC_HIP(dtc::launch_prep(P, ctx->stream));
-    for (size_t i = 0; i < n; ++i) {
-      const Launch& l = L[i0 + i];
+    for (size_t i = i0; i < i1; ++i) {
+      const Launch& l = L[i];
+      const dtc::KickRec* rec = P.out + (row0[i] - row0[i0]) * batch * dtc::kRecPerState;
       DTC_TRY(launch_pass_spec(ctx, rc, batch_start, batch, l.ps, l.src, l.dst, l.meas_mode,
-                               l.meas_at_end, l.n_obs, l.meas_out, l.meas_stride,
-                               P.out + i * batch * dtc::kRecPerState, 0, l.no_store, l.basis));
+                               l.meas_at_end, l.n_obs, l.meas_out, l.meas_stride, rec, 0,
+                               l.no_store, l.basis, 0,
+                               l.dst2 ? rec + batch * dtc::kRecPerState : nullptr, l.dst2));
     }
+    i0 = i1;
   }
   return DTC_OK;
 }
@@ -1185,6 +1209,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   // with the full passes, each form on its own engine)
   c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
   c->lc_wide = std::getenv("DTC_NO_LCW") == nullptr;
+  c->dual = std::getenv("DTC_NO_DUAL") == nullptr;
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1558,6 +1583,29 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         // the echo state is only measured: the chain's last pass reads its
         // tiles and stores nothing (the next chain starts from F again)
         sched.back().no_store = 1;
+        // Dual pass: the forward K-D-K on G just before the chain computes
+        // K_{p+1} D K_p (input); the chain's first pass, on the same G, is
+        // undo(K_{p+1}) D^* K'_1 of that -- so K'_1 K_p (input), which the
+        // forward pass forms from its own tile after the pre-kick and stores
+        // to E: the chain's first read of F and its own pass go away (48 B
+        // per amplitude instead of 64).  Not when the chain is one pass (the
+        // light-cone end reads F itself).
+        if (ctx->dual && !rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
+          Launch& f = sched[chain0 - 1];
+          const Launch& e = sched[chain0];
+          const bool fkdk = pass_shape(f.ps) == dtc::kShapeKDK && !f.basis && f.src == F;
+          const bool ekdk = pass_shape(e.ps) == dtc::kShapeKDK && e.ps.lc_w0 < 0 &&
+                            e.ps.group == f.ps.group && e.ps.pre.mode == dtc::kKickUndo &&
+                            e.ps.post.enabled && e.ps.pre.skip == 0 && f.ps.post.skip == 0;
+          const int fk = fkdk ? pass_kind(rc, f.ps, dtc::kShapeKDK) : -1;
+          const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};
+          if (fkdk && ekdk && (fk == dtc::kKindRX || fk == dtc::kKindRY || fk == dtc::kKindGen) &&
+              fk == pass_kind(rc, e.ps, dtc::kShapeKDK) && fk == pass_kind(rc, branch, -1)) {
+            f.ps2 = branch;
+            f.dst2 = E;
+            sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
+          }
+        }
       }
     }
     if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));

@@ -238,6 +238,10 @@ struct PassArgs {
   int lc_split, lc_tpb;    // light-cone pass variant (dev A/B, read once in dtc_open)
   int kdk_split;           // K-D-K at three workgroups per CU (dtc_kdk_pass3): bit NIBS for
                            // measurement classes 0/1, bit 8 + NIBS for 2/3
+  // non-null: a dual pass (dtc_kdk_dual) -- the tile after the pre-kick also
+  // takes recs2's post-kick (the echo chain's first layer) and goes to dst2
+  const KickRec* recs2;
+  double2* dst2;
   uint64_t* dbg_ts;        // development builds (-DDTC_PHASE_TIMING) only; null otherwise
 };
 

@@ -410,9 +410,17 @@ struct RoundPlan {
 // (per-site / energy Z), 3 = energy with the in-flight <X> points.
 // SPLIT: re-layouts through a 32 KiB half-tile buffer (exchange_split), so a
 // third workgroup fits a CU (dtc_kdk_pass3; development A/B, PassArgs::kdk_split)
-template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false, bool SPLIT = false>
+// DUAL (a forward K-D-K that also starts an echo branch, dtc_kdk_dual): after
+// the pre-kick the tile is copied; the copy takes the echo chain's first kick
+// layer (A.recs2's post-kick, its global factor A.recs2's total) and is stored
+// to A.dst2, then the pass goes on (diagonal, probe, post-kick, store to dst).
+template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false, bool SPLIT = false,
+          bool DUAL = false>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
+  static_assert(!DUAL || (SHAPE == kShapeKDK && MC <= 1 && !NS &&
+                          (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)),
+                "dual passes: unitary K-D-K, at most the probe");
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
 #ifdef DTC_PHASE_TIMING
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -448,6 +456,17 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       r1 = rp[1];
     }
     R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
+  RecRegs R2;  // DUAL: the echo branch's records (its post-kick and total)
+  if constexpr (DUAL) {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs2 + b * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < 8 * kRecPerState) {
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R2.rv[0] = r0.x; R2.rv[1] = r0.y; R2.rv[2] = r1.x; R2.rv[3] = r1.y;
   }
 
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
@@ -857,6 +876,38 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
   }
   DTC_TS(3);
+  if constexpr (DUAL) {
+    // the echo branch: E = K'_1 K_p (input) -- the forward pass's D, its
+    // post-kick K_{p+1} and the echo's D^* and undo of K_{p+1} cancel exactly
+    double2 w[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) w[r] = v[r];
+    if constexpr (RP::nO) {
+      xch_tile<SPLIT, RP::d_lay, RP::O>(w, s_tile, s_half, t);
+      apply_nibble<RP::O, KIND>(w, R2, kTileBits);
+    }
+    if constexpr (RP::n0) {
+      xch_tile<SPLIT, RP::pO, 0>(w, s_tile, s_half, t);
+      apply_nibble<0, KIND>(w, R2, kTileBits);
+    }
+    if constexpr (RP::nIO) {
+      xch_tile<SPLIT, RP::p0, RP::IO>(w, s_tile, s_half, t);
+      apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
+    }
+    xch_tile<SPLIT, RP::pIO, RP::IO>(w, s_tile, s_half, t);
+    // the branch's global factor: i^k w of K_p and of K'_1
+    const double2 gE = make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1));
+    char* d2 = (char*)(A.dst2 + sbase);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const double2 u = cmul(w[r], gE);
+      d2v x = {u.x, u.y};
+      __builtin_nontemporal_store(x, (d2v*)(d2 + tile_ofs(r) + (ofs32 ? (int64_t)vofs : vofs64)));
+    }
+    // the forward's next re-layout writes slots other threads may still be
+    // reading in the branch's last one
+    __syncthreads();
+  }
   if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0);
   if constexpr (!RP::diag) {
     // no diagonal to carry the kicks' global factor (kick-only pass: no
@@ -1010,6 +1061,13 @@ template <int NIBS, int KIND, int MC>
 __global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
   pass_body<kShapeKDK, NIBS, KIND, MC, false, true>(A);
 }
+// a forward K-D-K that also starts an echo branch (pass_body DUAL): two
+// tiles in registers, so two workgroups per CU; half-tile re-layouts (their
+// opaque per-thread bases keep the addresses out of the register budget)
+template <int NIBS, int KIND, int MC>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kdk_dual(PassArgs A) {
+  pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true>(A);
+}
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
 DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
@@ -1056,6 +1114,15 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
+    }
+  }
+  if (a.dst2) {
+    if constexpr (MC <= 1 && (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) {
+      if (shape != kShapeKDK) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
     }
   }
   switch (shape) {

@@ -280,6 +280,44 @@ def test_lcw2_c2_form(pkg, monkeypatch, L, pol, state, toff, g, p):
     assert np.abs(got["echo"] - narrow["echo"]).max() < 1e-12
 
 
+@pytest.mark.parametrize("L,T,pol,state,toff,p", [
+    (20, 12, "x", "vacuum", 0, 0.05),     # C2's kicks: 12 + 8 site groups
+    (16, 10, "y", "neel", 1, 0.1),
+    (13, 9, "circular_left", "vacuum", 0, 0.1),   # general 2x2 kicks
+    (22, 8, "x", "neel", 0, 0.05),        # three site groups
+])
+def test_dual_pass_echo_start(pkg, monkeypatch, L, T, pol, state, toff, p):
+    """An echo chain's first pass folded into the forward K-D-K before it
+    (dtc_kdk_dual: the tile after the pre-kick K_p also takes the chain's first
+    inverse layer and goes to E, since undo(K_{p+1}) D^* D K_p = K_p): per
+    trajectory the oracle's values (1e-10), the unfused schedule's
+    (DTC_NO_DUAL) to 1e-12, and fewer K-D-K launches."""
+    rng = np.random.default_rng(L * 5 + T)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, noise_prob=p, polarization=pol,
+                         initial_state=state, t_offset=toff)
+
+    def run(no_dual):
+        with monkeypatch.context() as m:
+            if no_dual:
+                m.setenv("DTC_NO_DUAL", "1")
+            with pkg.DtcEngine(0) as eng:
+                eng.set_profiling(True)
+                out = eng.autocorr(spec, 3, seed=19)
+                st = eng.kernel_stats()
+        return out, st[pkg._capi.KERNEL_LO_PASS]
+
+    got, lo = run(False)
+    ref, lo_ref = run(True)
+    _cmp(got, c_oracle.autocorr(spec, 3, seed=19))
+    assert np.abs(got["echo"] - ref["echo"]).max() < 1e-12
+    assert np.abs(got["fwd"] - ref["fwd"]).max() < 1e-13
+    assert lo["launches"] < lo_ref["launches"], (lo, lo_ref)
+    # a dual pass moves 48 B per amplitude: 16 fewer than its two passes
+    n_dual = lo_ref["launches"] - lo["launches"]
+    assert lo["bytes"] == pytest.approx(lo_ref["bytes"] - n_dual * 16.0 * 3 * (1 << max(L, 12)))
+
+
 def test_independent_t_matches_oracle(pkg, engine):
     """--independent_t: every t from its own trajectories (t_first runs of
     t + t_offset periods, fast.py:219-221) -- engine = C oracle per trajectory."""
