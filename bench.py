@@ -802,6 +802,9 @@ def main_c5(args):
     pass_ms = (lo_s["total_ms"] + hi_s["total_ms"]) / n_per
     pass_bytes = (lo_s["bytes"] + hi_s["bytes"]) / n_per
     sent = shard_bytes * (W - 1) / W   # per rank per period (in place: moved per GPU)
+    # in place on one GPU the slices' exchange is fused into their last kick
+    # pass (dtc_shard_kick_exchange_slice): no kernel of its own, no window
+    fused = inplace and xk["launches"] == 0
     if inplace:
         xch_ms = xk["total_ms"] / n_per          # the swap kernels (engine HIP events)
     else:
@@ -848,16 +851,20 @@ def main_c5(args):
         "launches_per_period": {"kdk_pass": lo_s["launches"] / n_per,
                                 "kick_pass": hi_s["launches"] / n_per,
                                 "exchange": xk["launches"] / n_per},
-        "exchange": {"per_period_ms": xch_ms,
+        "exchange": {"per_period_ms": xch_ms, "fused_into_kick_pass": fused,
                      "bytes_per_period_per_rank": sent,
                      "swap_kernel_hbm_GBps": (xk["bytes"] / (xk["total_ms"] / 1e3) / 1e9
                                               if inplace and xk["total_ms"] else None),
                      "GBps_per_rank": sent / (xch_ms / 1e3) / 1e9 if xch_ms > 0 else None,
-                     "window": ("the swap kernels' HIP events (engine stream; serial with the "
+                     "window": ("none: each slice's last kick pass stores every piece at its "
+                                "partner's place (dtc_shard_kick_exchange_slice)" if fused else
+                                "the swap kernels' HIP events (engine stream; serial with the "
                                 "kicks)" if inplace else
                                 "side-stream events from the first slice's transfer to the last "
                                 "one's completion (overlaps the slice kicks)"),
-                     "kind": ("in-place piece swap per slice (virtual ranks, one 256 GiB "
+                     "kind": ("in-place piece swap fused into the slice kicks (virtual ranks, "
+                              "one 256 GiB buffer)" if fused else
+                              "in-place piece swap per slice (virtual ranks, one 256 GiB "
                               "buffer: dtc_shard_exchange_slice)" if inplace else
                               "strided device copy per slice (virtual ranks)" if world == 1 else
                               "RCCL point-to-point per slice over xGMI: every peer at once "

@@ -1593,7 +1593,9 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         if (ctx->dual && !rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
           Launch& f = sched[chain0 - 1];
           const Launch& e = sched[chain0];
-          const bool fkdk = pass_shape(f.ps) == dtc::kShapeKDK && !f.basis && f.src == F;
+          // (the dual kernel carries the probe at most: not with per-site Z)
+          const bool fkdk = pass_shape(f.ps) == dtc::kShapeKDK && !f.basis && f.src == F &&
+                            (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
           const bool ekdk = pass_shape(e.ps) == dtc::kShapeKDK && e.ps.lc_w0 < 0 &&
                             e.ps.group == f.ps.group && e.ps.pre.mode == dtc::kKickUndo &&
                             e.ps.post.enabled && e.ps.pre.skip == 0 && f.ps.post.skip == 0;

@@ -637,16 +637,9 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
   // global bit of each window site; the tile's base (its id deposited into
   // the bits off the window, as lc_merge_wide's lc_gb)
   auto gpos = [&](int s) { return s == c0 ? 0 : (s == c1 ? 1 : j + off_of(s)); };
-  const uint32_t win = 3u | (0x3FFu << (j - 5));
-  uint32_t tbase = 0;
-  {
-    uint32_t rest = (uint32_t)tile;
-    for (int g = 0; g < A.L_eff; ++g) {
-      if ((win >> g) & 1u) continue;
-      tbase |= (rest & 1u) << g;
-      rest >>= 1;
-    }
-  }
+  // (the bits off the window are 2 .. j-6 and j+5 .. L_eff-1: two shifts)
+  const uint32_t tbase = (((uint32_t)tile & ((1u << (j - 7)) - 1u)) << 2) |
+                         (((uint32_t)tile >> (j - 7)) << (j + 5));
   const int bit_p5 = (int)((tbase >> (j + 5)) & 1u);  // table 5b's bit j+5
   double2 v[kRegs];  // the tile: 16 amplitudes per thread
   // re-layout through the 4108-slot half buffer (real parts, then imaginary)
@@ -694,14 +687,19 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
     for (int p = 4; p < 12; ++p) xl |= (uint32_t)((t >> (p - 4)) & 1) << gpos(lay_site(kL0, p));
     const int64_t vofs = octet_spread((int64_t)xl, og) << 4;
     const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
+    // register offsets: the spread is linear over disjoint bits, so one per
+    // register bit, summed (uniform)
+    const int64_t sp0 = octet_spread((int64_t)tbase, og) << 4;
+    int64_t spq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) spq[q] = octet_spread((int64_t)1 << gpos(lay_site(kL0, q)), og) << 4;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      uint32_t xr = tbase;
+      int64_t o = sp0;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if ((r >> q) & 1) xr |= 1u << gpos(lay_site(kL0, q));
-      const char* a = src + (octet_spread((int64_t)xr, og) << 4) + vofs;
-      const d2v w = __builtin_nontemporal_load((const d2v*)a);
+        if ((r >> q) & 1) o += spq[q];
+      const d2v w = __builtin_nontemporal_load((const d2v*)(src + o + vofs));
       v[r] = make_double2(w.x, w.y);
     }
   }

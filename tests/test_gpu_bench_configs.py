@@ -64,4 +64,5 @@ def test_c5_subrun_forced():
     assert "error" not in d["c5"], d["c5"]
     assert d["c5"]["config"]["shards"] == 8
     assert abs(d["c5"]["z_t1_mean"] - COS) < 1e-12
-    assert d["c5"]["exchange"]["per_period_ms"] > 0
+    # (in place on one GPU the exchange is fused into the slice kicks: no window)
+    assert d["c5"]["exchange"]["per_period_ms"] > 0 or d["c5"]["exchange"]["fused_into_kick_pass"]
