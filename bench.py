@@ -687,6 +687,9 @@ def main_c4(args):
     launch_bytes = lo_s["bytes"] / max(1, lo_s["launches"])
     hi_bytes = hi_s["bytes"] / max(1, hi_s["launches"])
     achieved = launch_bytes / avg_lo / 1e9 if lo_s["launches"] else 0.0
+    # PMC summary of this config (tools/pmc_traffic.sh with BENCH_ARGS="--config
+    # c4", L=28): one launch holds the step's n instances' states
+    traffic, traffic_src = read_traffic(launch_bytes, "_pmc_c4.json", batch=n)
     res = {
         "metric": "Floquet-periods×instances/sec at L=28 (C4); RZZ-kernel HBM GB/s vs peak",
         "value": value, "unit": "periods*instances/s", "n_gpus": world, "steps": args.steps,
@@ -701,7 +704,8 @@ def main_c4(args):
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "frac_of_best_rw_stream": achieved / BEST_RW_STREAM_GBS,
-                     "traffic": None, "algorithmic_bytes_per_launch": launch_bytes,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": launch_bytes,
                      "avg_launch_ms": avg_lo * 1e3, "launches": lo_s["launches"]},
         "kernels": {"kdk_pass": {"launches": lo_s["launches"], "avg_ms": avg_lo * 1e3},
                     "kick_pass": {"launches": hi_s["launches"], "avg_ms": avg_hi * 1e3,

@@ -181,27 +181,25 @@ __device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, i
 // The same re-layout through a half-tile buffer, real parts then imaginary
 // parts (8-B slots): about half the LDS, so three workgroups fit a CU; two
 // more barriers (the imaginary writes reuse the slots the real reads just
-// left).  Slots are additive in the tile index's nibbles,
-//   slot(y) = y[0:4) + 17 y[4:8) + 272 y[8:12)   (4351 slots, 34.8 KB),
-// so a slot is the thread's base plus a compile-time register offset -- the
-// ds_write_b64 / ds_read_b64 immediate, no address VALU per access (the XOR
-// swizzle it replaces cost one per access: 256 VALU per wave in a 12-site
-// K-D-K).  Conflict-free: the lane bits 0..3 of every layout (tile bits 0..3 in
-// layouts 1 and 2, 4..7 in layout 0) weigh 1, 2, 4, 8 mod 16 -- distinct
-// banks in every 16-lane group -- and lane bits 0..4 of layouts 0 and 1 weigh
-// 2^0 .. 2^4 times an odd number mod 32 (layout 2's lane bit 4 weighs 17: one
-// bank pair shared by two lanes of a 32-lane ds_read_b64 group; the compiler
-// merges these reads into ds_read2_b64, whose groups are 16 lanes).
-#ifndef DTC_XOR_SLOTS
+// left).  Slots are the tile index XOR-swizzled,
+//   slot(y) = y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4),
+// linear over XOR, so a slot is the thread's base XOR a compile-time register
+// offset (one VALU op per access); the compiler merges register pairs into
+// ds_read2_b64 / ds_write2st64_b64.  Development builds with -DDTC_ADD_SLOTS
+// use additive slots, y[0:4) + 17 y[4:8) + 272 y[8:12) (4351 slots): base +
+// immediate offset, no address VALU, but either merged into ds_read2 pairs or
+// (Makefile KNOMERGE=1) issued one by one they ran slower on the same box --
+// C2 -2.0 % (r4c, merged) and -1.9 % (r4d, unmerged), energy -2.4 %.
+#ifdef DTC_ADD_SLOTS
 static constexpr int kHalfSlots = 15 + 17 * 15 + 272 * 15 + 1;
 __host__ __device__ constexpr int slot_add(int y) {
   return (y & 15) + 17 * ((y >> 4) & 15) + 272 * (y >> 8);
 }
+#define DTC_SLOT(base, LAY, r) ((base) + slot_add((r) << (4 * (LAY))))
 #else
-// development A/B build (-DDTC_XOR_SLOTS): the round-3 XOR swizzle
-// y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4), one VALU op per access
 static constexpr int kHalfSlots = kTile;
 __host__ __device__ constexpr int slot_add(int y) { return y ^ ((y >> 4) & 15) ^ (((y >> 8) & 1) << 4); }
+#define DTC_SLOT(base, LAY, r) ((base) ^ slot_add((r) << (4 * (LAY))))
 #endif
 template <int FROM, int TO>
 __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t) {
@@ -212,11 +210,6 @@ __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_ha
   // for 16 slot addresses per layout, r3h)
   int bf = slot_add(ybase<FROM>(t)), bt = slot_add(ybase<TO>(t));
   asm volatile("" : "+v"(bf), "+v"(bt));
-#ifndef DTC_XOR_SLOTS
-#define DTC_SLOT(base, LAY, r) ((base) + slot_add((r) << (4 * (LAY))))
-#else
-#define DTC_SLOT(base, LAY, r) ((base) ^ slot_add((r) << (4 * (LAY))))
-#endif
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) s_half[DTC_SLOT(bf, FROM, r)] = v[r].x;
   __syncthreads();
@@ -228,7 +221,6 @@ __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_ha
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) v[r].y = s_half[DTC_SLOT(bt, TO, r)];
-#undef DTC_SLOT
 }
 
 template <bool SPLIT, int FROM, int TO>

@@ -685,6 +685,20 @@ struct Launch {
 
 int run_launches(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int batch,
                  const std::vector<Launch>& L) {
+#ifdef DTC_DEV_KNOBS
+  // development builds: DTC_PRINT_SCHED=1 lists the batch's schedule on stderr
+  if (std::getenv("DTC_PRINT_SCHED")) {
+    auto role = [&](const void* p) {
+      return p == ctx->F.p ? "F" : (p == ctx->E.p ? "E" : (p ? "?" : "-"));
+    };
+    for (size_t i = 0; i < L.size(); ++i)
+      std::fprintf(stderr, "sched %zu g%d shape%d diag%d pre%d post%d lc%d %s->%s%s meas%d%s%s\n", i,
+                   L[i].ps.group, pass_shape(L[i].ps), L[i].ps.diag, L[i].ps.pre.enabled,
+                   L[i].ps.post.enabled, L[i].ps.lc_w0, role(L[i].src), role(L[i].dst),
+                   L[i].dst2 ? "+E" : "", L[i].meas_mode, L[i].no_store ? " nostore" : "",
+                   L[i].basis ? " basis" : "");
+  }
+#endif
   // one record row per launch, two for a dual pass (its echo branch's kicks)
   std::vector<size_t> row0(L.size() + 1);
   ctx->pk_host.clear();

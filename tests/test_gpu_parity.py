@@ -317,9 +317,10 @@ def test_dual_pass_echo_start(pkg, monkeypatch, L, T, pol, state, toff, p):
     assert np.abs(got["echo"] - ref["echo"]).max() < 1e-12
     assert np.abs(got["fwd"] - ref["fwd"]).max() < 1e-13
     assert lo["launches"] < lo_ref["launches"], (lo, lo_ref)
-    # a dual pass moves 48 B per amplitude: 16 fewer than its two passes
+    # a dual pass moves 48 B per amplitude, 16 fewer than its two passes
+    # (2 instances x 3 trajectories per launch)
     n_dual = lo_ref["launches"] - lo["launches"]
-    assert lo["bytes"] == pytest.approx(lo_ref["bytes"] - n_dual * 16.0 * 3 * (1 << max(L, 12)))
+    assert lo["bytes"] == pytest.approx(lo_ref["bytes"] - n_dual * 16.0 * 6 * (1 << max(L, 12)))
 
 
 def test_independent_t_matches_oracle(pkg, engine):
@@ -344,3 +345,4 @@ def test_independent_t_matches_oracle(pkg, engine):
     ref = pkg.sweep.autocorr_independent_t(Oracle(), spec, n, seed=5)
     for k in ("fwd", "echo"):
         assert np.abs(got[k] - ref[k]).max() < 1e-10
+

@@ -1,0 +1,30 @@
+# r4e: HEAD re-profile (XOR slots + dual pass as the product): the dual pass's
+# schedule/byte probe (development library), then C2 (bench + kernel stats +
+# PMC), and C4 / C3 / energy each with bench, kernel stats and PMC traffic at
+# the line's own batch; ctrl and C5 bench lines.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT
+O=gpurun_out
+for a in "13 9 circular_left vacuum 0 0.1" "20 12 x vacuum 0 0.05"; do
+  for m in dual no_dual; do
+    f=$O/r4e_probe_$(echo $a | tr ' ' '_')_$m.txt
+    DTC_LIB=$R/devlib/dev.so timeout -k 10 120 python tools/dual_sched_probe.py $a $m > $f 2>&1 || { tail -5 $f; exit 1; }
+    grep "^kind" $f
+  done
+done
+bash tools/measure_c2.sh r4e || exit 1
+export TMPDIR=/tmp
+for c in c4 c3 energy; do
+  timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline > $O/r4e_${c}_bench.json 2> $O/r4e_${c}_bench.err || { tail -5 $O/r4e_${c}_bench.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/r4e_${c}_bench.json')); r=d['roofline']; print('$c', round(d['value'], 2), round(r['achieved']), r.get('avg_launch_ms'), d.get('kernels'))"
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_r4e_$c -o kt -- python $R/bench.py --config $c --no-cpu-baseline --steps 2 --warmup 1 > $R/$O/prof_r4e_${c}.log 2>&1) || { echo "$c trace failed"; exit 1; }
+done
+L=28 BENCH_ARGS="--config c4" SUFFIX=_pmc_c4 bash tools/pmc_traffic.sh r4e 32 || exit 1
+BENCH_ARGS="--config c3" SUFFIX=_pmc_c3 bash tools/pmc_traffic.sh r4e 1024 || exit 1
+BENCH_ARGS="--config energy" SUFFIX=_pmc_energy bash tools/pmc_traffic.sh r4e 1024 || exit 1
+for c in ctrl c5; do
+  timeout -k 10 400 python -u bench.py --config $c --no-cpu-baseline > $O/r4e_${c}_bench.json 2> $O/r4e_${c}_bench.err || { tail -5 $O/r4e_${c}_bench.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/r4e_${c}_bench.json')); print('$c', round(d['value'], 2))"
+done
+echo ok

@@ -21,23 +21,50 @@ def main(prof, out, batch, L, bench_args=""):
     res = {"source": prof, "batch": batch, "L": L, "bench_args": bench_args,
            "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 FETCH_SIZE halving"}
     amps = float(1 << max(L, 12)) * batch
-    for kname, key in (("dtc_kdk_pass", "lo_pass"), ("dtc_kick_pass", "hi_pass"),
-                       ("dtc_lc_final", "lightcone_pass"),
-                       ("dtc_lcw_final", "lightcone_wide_pass")):
-        fsel = fe[fe.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
-        wsel = wr[wr.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
-        if not len(fsel) or not len(wsel):
-            continue
-        f = fsel.mean() * 1024
-        w = wsel.mean() * 1024
-        hbm = 2 * f + w
-        reads = 2 * f > 0.01 * hbm
-        writes = w > 0.01 * hbm
-        alg = (16.0 * (int(reads) + int(writes))) * amps
-        res[key] = {"kernel": kname, "launches": int(len(fsel)), "fetch_bytes_raw": f,
-                    "write_bytes": w, "hbm_bytes_per_launch": hbm,
-                    "algorithmic_bytes_per_launch": alg,
-                    "ratio_to_algorithmic": hbm / alg}
+
+    def one(names, per_amp=None):
+        """launch-weighted totals over the kernels whose names contain any of
+        `names`; per_amp = algorithmic bytes per amplitude by name (None: 16 B
+        per direction the counters show)"""
+        n = 0
+        f_tot = w_tot = alg_tot = 0.0
+        for kname in names:
+            fsel = fe[fe.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
+            wsel = wr[wr.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
+            if not len(fsel) or not len(wsel):
+                continue
+            f, w = fsel.mean() * 1024, wsel.mean() * 1024
+            hbm = 2 * f + w
+            if per_amp and kname in per_amp:
+                a = per_amp[kname] * amps
+            else:
+                a = 16.0 * (int(2 * f > 0.01 * hbm) + int(w > 0.01 * hbm)) * amps
+            k = len(fsel)
+            n += k
+            f_tot += f * k
+            w_tot += w * k
+            alg_tot += a * k
+        if not n:
+            return None
+        hbm = (2 * f_tot + w_tot) / n
+        return {"kernel": " + ".join(names), "launches": n, "fetch_bytes_raw": f_tot / n,
+                "write_bytes": w_tot / n, "hbm_bytes_per_launch": hbm,
+                "algorithmic_bytes_per_launch": alg_tot / n,
+                "ratio_to_algorithmic": hbm / (alg_tot / n)}
+
+    # the K-D-K passes as the bench line aggregates them: dtc_kdk_pass /
+    # dtc_kdk_pass3 (32 B per amplitude) and the dual forward+echo-start
+    # dtc_kdk_dual (48 B: one read, two stores)
+    for key, names, per_amp in (
+            ("lo_pass", ("dtc_kdk_pass", "dtc_kdk_dual"), {"dtc_kdk_pass": 32.0, "dtc_kdk_dual": 48.0}),
+            ("kdk_single", ("dtc_kdk_pass",), {"dtc_kdk_pass": 32.0}),
+            ("kdk_dual", ("dtc_kdk_dual",), {"dtc_kdk_dual": 48.0}),
+            ("hi_pass", ("dtc_kick_pass",), None),
+            ("lightcone_pass", ("dtc_lc_final",), None),
+            ("lightcone_wide_pass", ("dtc_lcw2_final", "dtc_lcw_final"), None)):
+        r = one(names, per_amp)
+        if r:
+            res[key] = r
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
