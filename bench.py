@@ -556,8 +556,11 @@ def main(argv=None):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("dtc_kdk_pass (kick layer . fused RZZ+RZ diagonal . kick layer; one "
-                       "launch advances every state by one Floquet period)"),
+            "kernel": ("dtc_kdk_pass / dtc_kdk_pass3 / dtc_kdk_dual (kick layer . fused RZZ+RZ "
+                       "diagonal . kick layer; one launch advances every state by one Floquet "
+                       "period; the dual form also stores the echo branch's first pass, 48 B "
+                       "per amplitude, so the per-launch algorithmic bytes average above "
+                       "32 * 2^L * B); launch-weighted over all of them"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -872,7 +875,14 @@ def main_c5(args):
                               "buffer: dtc_shard_exchange_slice)" if inplace else
                               "strided device copy per slice (virtual ranks)" if world == 1 else
                               "RCCL point-to-point per slice over xGMI: every peer at once "
-                              "(batch_isend_irecv of 7 sends + 7 receives)")},
+                              "(batch_isend_irecv of 7 sends + 7 receives)"),
+                     # what has checked this exchange before this run
+                     "verification": ("virtual ranks on one GPU: tests/test_gpu_c5_l34.py, "
+                                      "test_gpu_sharded.py" if world == 1 else
+                                      "unverified on GPUs before this run: the real-rank "
+                                      "ordering ran over the loopback transport "
+                                      "(test_loopback_real_rank_exchange) and gloo (world 8), "
+                                      "RCCL itself only here; check z_t1_mean = cos(pi g)")},
         "per_rank": [{"rank": i, "period_ms": float(r[0]), "pass_ms": float(r[1]),
                       "exchange_ms": float(r[2]), "exchange_GBps": float(r[3])}
                      for i, r in enumerate(ranks)],

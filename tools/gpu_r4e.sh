@@ -1,18 +1,10 @@
-# r4e: HEAD re-profile (XOR slots + dual pass as the product): the dual pass's
-# schedule/byte probe (development library), then C2 (bench + kernel stats +
-# PMC), and C4 / C3 / energy each with bench, kernel stats and PMC traffic at
-# the line's own batch; ctrl and C5 bench lines.
+# r4e: HEAD re-profile (XOR slots + dual pass as the product): C2 (bench +
+# kernel stats + PMC), C4 / C3 / energy each with bench, kernel stats and PMC
+# traffic at the line's own batch; ctrl and C5 bench lines; the GPU suite.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 R=$GRAFT_REPO_ROOT
 O=gpurun_out
-for a in "13 9 circular_left vacuum 0 0.1" "20 12 x vacuum 0 0.05"; do
-  for m in dual no_dual; do
-    f=$O/r4e_probe_$(echo $a | tr ' ' '_')_$m.txt
-    DTC_LIB=$R/devlib/dev.so timeout -k 10 120 python tools/dual_sched_probe.py $a $m > $f 2>&1 || { tail -5 $f; exit 1; }
-    grep "^kind" $f
-  done
-done
 bash tools/measure_c2.sh r4e || exit 1
 export TMPDIR=/tmp
 for c in c4 c3 energy; do
@@ -27,4 +19,7 @@ for c in ctrl c5; do
   timeout -k 10 400 python -u bench.py --config $c --no-cpu-baseline > $O/r4e_${c}_bench.json 2> $O/r4e_${c}_bench.err || { tail -5 $O/r4e_${c}_bench.err; exit 1; }
   python -c "import json; d=json.load(open('$O/r4e_${c}_bench.json')); print('$c', round(d['value'], 2))"
 done
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/r4e_gputest.txt 2>&1; rc=$?
+tail -6 $O/r4e_gputest.txt
+[ $rc -le 1 ] || exit $rc
 echo ok

@@ -1,0 +1,24 @@
+# r4g: the light-cone pass's PMC excess (r4e: dtc_lcw2_final FETCH_SIZE x2 = 1.44 x its
+# algorithmic bytes): read-only microbenchmark of its load pattern (64-B runs) against
+# 128-B / 256-B runs and contiguous tiles, timed and under a FETCH_SIZE pass; then the
+# SQ counters of the C2 pass kernels at HEAD (tools/pmc_sq.sh).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT
+O=gpurun_out
+timeout -k 10 120 ./tools/run64_bench > $O/r4g_run64.txt 2>&1 || { cat $O/r4g_run64.txt; exit 1; }
+cat $O/r4g_run64.txt
+export TMPDIR=/tmp
+(cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$O/pmc_r4g_run64 -o fetch -- $R/tools/run64_bench > $R/$O/pmc_r4g_run64.log 2>&1) || { echo "fetch pass failed"; tail -5 $O/pmc_r4g_run64.log; exit 1; }
+python - <<'PY'
+import glob, pandas as pd
+f = glob.glob("gpurun_out/pmc_r4g_run64/**/fetch_counter_collection.csv", recursive=True)[0]
+d = pd.read_csv(f)
+g = d.groupby("Kernel_Name").Counter_Value.mean() * 1024 / (16 * 2**30)
+print("FETCH_SIZE per launch / 16 GiB read:")
+print(g.to_string())
+PY
+bash tools/pmc_sq.sh r4g || exit 1
+python tools/sq_table.py gpurun_out/pmc_r4g > $O/r4g_sq_table.md || exit 1
+cat $O/r4g_sq_table.md
+echo ok
