@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
       const char* a = src + (octet_spread((int64_t)(tbase | reg_part(L2{}, r)), og) << 4) + vofs;
-      const d2v w = __builtin_nontemporal_load((const d2v*)a);
+      const d2v w = *(const d2v*)a;  // ordinary load: 64-B runs (note above dtc_lcw2_final)
       v[r] = make_double2(w.x, w.y);
     }
   }
@@ -476,6 +476,17 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
     A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
   }
 }
+
+// Tile loads of the 10-site passes (dtc_lcw_final, dtc_lcw2_final) are
+// ordinary, not nontemporal: their tiles read 64-B runs (global bits 0, 1),
+// so each 128-B line's other half belongs to the partner tile (global bit 2,
+// the next block on the same XCD).  With the nontemporal hint L2 does not keep
+// the line for it and HBM serves it twice: tools/run64_bench.hip (r4g) reads
+// that pattern at 4.45-4.67 TB/s, FETCH_SIZE x2 = 1.38 x the bytes, against
+// 5.68-5.91 TB/s and x1.02 with ordinary loads; the pass's own PMC went
+// x1.44 -> x1.0001 and its time 5.61 -> 5.43 ms (same box).  Runs of 128 B
+// and more keep the nontemporal hint (no partner: x1.000 either way, and
+// faster: 256-B runs 6.96 vs 6.59 TB/s).
 
 // ---- the 10-site light-cone end, C2 form (dtc_lcw2_final) ------------------
 // The same six layers on the same window as dtc_lcw_final (kLcwMaskJ2, the
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if ((r >> q) & 1) o += spq[q];
-      const d2v w = __builtin_nontemporal_load((const d2v*)(src + o + vofs));
+      const d2v w = *(const d2v*)(src + o + vofs);  // ordinary load (note above this section)
       v[r] = make_double2(w.x, w.y);
     }
   }

@@ -1,4 +1,5 @@
-// Read-only access patterns of the light-cone passes (development tool).
+// Read-only access patterns of the light-cone passes (development tool),
+// with nontemporal and with ordinary loads.
 // 1024 L=20 states in the octet layout (16 GiB); each 256-thread workgroup
 // reads one 4096-amplitude tile of one state, 16 amplitudes per lane, with
 // nontemporal 16-B loads, and reduces them (one double per workgroup, so
@@ -55,7 +56,7 @@ struct Pat<3> {
   static constexpr int id[8] = {12, 13, 14, 15, 16, 17, 18, 19};
 };
 
-template <int P>
+template <int P, bool NT>
 __global__ __launch_bounds__(256) void k_read(const double2* __restrict__ src, double* out) {
   using T = Pat<P>;
   const int t = threadIdx.x;
@@ -76,7 +77,8 @@ __global__ __launch_bounds__(256) void k_read(const double2* __restrict__ src, d
     int64_t y = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) y |= (int64_t)((r >> i) & 1) << T::reg[i];
-    const d2v w = __builtin_nontemporal_load((const d2v*)(base + (spread(y) << 4) + vofs));
+    const d2v* a = (const d2v*)(base + (spread(y) << 4) + vofs);
+    const d2v w = NT ? __builtin_nontemporal_load(a) : *a;
     acc += w.x + w.y;
   }
   if (acc == 12345.678) out[blockIdx.x + blockIdx.y * gridDim.x] = acc;  // keeps the loads
@@ -93,15 +95,20 @@ int main() {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const dim3 grid(8 * 256, kStates / 8), block(256);
-  const char* names[4] = {"R64  (lcw2 load: 64-B runs)", "R128 (128-B runs)", "R256 (256-B runs)",
-                          "RC   (contiguous tiles)"};
+  const char* names[8] = {"R64  nt (lcw2 load: 64-B runs)", "R128 nt (128-B runs)",
+                          "R256 nt (256-B runs)", "RC   nt (contiguous tiles)",
+                          "R64  temporal", "R128 temporal", "R256 temporal", "RC   temporal"};
   for (int rep = 0; rep < 2; ++rep) {
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < 8; ++p) {
       auto launch = [&]() {
-        if (p == 0) hipLaunchKernelGGL(k_read<0>, grid, block, 0, 0, s, out);
-        if (p == 1) hipLaunchKernelGGL(k_read<1>, grid, block, 0, 0, s, out);
-        if (p == 2) hipLaunchKernelGGL(k_read<2>, grid, block, 0, 0, s, out);
-        if (p == 3) hipLaunchKernelGGL(k_read<3>, grid, block, 0, 0, s, out);
+        if (p == 0) hipLaunchKernelGGL((k_read<0, true>), grid, block, 0, 0, s, out);
+        if (p == 1) hipLaunchKernelGGL((k_read<1, true>), grid, block, 0, 0, s, out);
+        if (p == 2) hipLaunchKernelGGL((k_read<2, true>), grid, block, 0, 0, s, out);
+        if (p == 3) hipLaunchKernelGGL((k_read<3, true>), grid, block, 0, 0, s, out);
+        if (p == 4) hipLaunchKernelGGL((k_read<0, false>), grid, block, 0, 0, s, out);
+        if (p == 5) hipLaunchKernelGGL((k_read<1, false>), grid, block, 0, 0, s, out);
+        if (p == 6) hipLaunchKernelGGL((k_read<2, false>), grid, block, 0, 0, s, out);
+        if (p == 7) hipLaunchKernelGGL((k_read<3, false>), grid, block, 0, 0, s, out);
       };
       launch();
       CHECK(hipDeviceSynchronize());
@@ -112,7 +119,7 @@ int main() {
       float ms = 0;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       ms /= 5;
-      printf("%-30s %8.3f ms  %6.0f GB/s (16 GiB read)\n", names[p], ms, bytes / (ms * 1e-3) / 1e9);
+      printf("%-34s %8.3f ms  %6.0f GB/s (16 GiB read)\n", names[p], ms, bytes / (ms * 1e-3) / 1e9);
     }
   }
   CHECK(hipFree(s));
