@@ -141,8 +141,17 @@ static int orc_device_draw(const orc_rng* r, uint64_t traj, uint32_t stream, uin
 }
 
 /* ---- gates on a 2^L statevector (bit i = site i) ------------------------ */
+/* States of 2^22 amplitudes and more (the L = 28 parity runs) are swept by
+ * all threads, one trajectory at a time (autocorr_run does not split such
+ * runs over trajectories); the loops are element-wise, so the result does not
+ * depend on the thread count, except measure_z's sums (per-thread partials
+ * added in thread order). */
+#define ORC_INNER_PAR(n) ((n) >= ((size_t)1 << 22))
 static void gate_1q(cpx* psi, int L, int site, const cpx m[4]) {
   const size_t n = (size_t)1 << L, bit = (size_t)1 << site;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) if (ORC_INNER_PAR(n))
+#endif
   for (size_t x = 0; x < n; ++x) {
     if (x & bit) continue;
     cpx a = psi[x], b = psi[x | bit];
@@ -165,6 +174,9 @@ static void gate_rzz(cpx* psi, int L, int i, int j, double theta) {
   const size_t n = (size_t)1 << L;
   const cpx same = cx(cos(-theta / 2), sin(-theta / 2));
   const cpx diff = cconj(same);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) if (ORC_INNER_PAR(n))
+#endif
   for (size_t x = 0; x < n; ++x) {
     int zz = (((x >> i) ^ (x >> j)) & 1) ? -1 : 1;
     psi[x] = cmul(psi[x], zz > 0 ? same : diff);
@@ -176,6 +188,9 @@ static void gate_rz(cpx* psi, int L, int i, double theta) {
   const size_t n = (size_t)1 << L;
   const cpx up = cx(cos(-theta / 2), sin(-theta / 2));
   const cpx dn = cconj(up);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) if (ORC_INNER_PAR(n))
+#endif
   for (size_t x = 0; x < n; ++x) psi[x] = cmul(psi[x], ((x >> i) & 1) ? dn : up);
 }
 
@@ -255,6 +270,35 @@ static void period_inverse(const orc_problem* pr, const orc_rng* rng, int inst, 
 static void measure_z(const cpx* psi, int L, double* out /* [1+L] */) {
   const size_t n = (size_t)1 << L;
   for (int i = 0; i <= L; ++i) out[i] = 0.0;
+#ifdef _OPENMP
+  if (ORC_INNER_PAR(n)) {
+    const int nt = omp_get_max_threads();
+    double* part = (double*)calloc((size_t)nt * (L + 1), sizeof(double));
+    if (part) {
+#pragma omp parallel num_threads(nt)
+      {
+        // blocks of 4096 amplitudes summed on their own, then added to the
+        // thread's partial: no long running sums (the GPU reduces in trees)
+        double* o = part + (size_t)omp_get_thread_num() * (L + 1);
+        double blk[65];
+#pragma omp for schedule(static)
+        for (size_t x0 = 0; x0 < n; x0 += 4096) {
+          for (int i = 0; i <= L; ++i) blk[i] = 0.0;
+          for (size_t x = x0; x < x0 + 4096; ++x) {
+            const double p = psi[x].re * psi[x].re + psi[x].im * psi[x].im;
+            blk[0] += p;
+            for (int i = 0; i < L; ++i) blk[1 + i] += ((x >> i) & 1) ? -p : p;
+          }
+          for (int i = 0; i <= L; ++i) o[i] += blk[i];
+        }
+      }
+      for (int t = 0; t < nt; ++t)
+        for (int i = 0; i <= L; ++i) out[i] += part[(size_t)t * (L + 1) + i];
+      free(part);
+      return;
+    }
+  }
+#endif
   for (size_t x = 0; x < n; ++x) {
     double p = psi[x].re * psi[x].re + psi[x].im * psi[x].im;
     out[0] += p;
@@ -303,7 +347,7 @@ static int autocorr_run(const orc_problem* pr, const orc_rng* rngp, double fac, 
   int err = 0;
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
-#pragma omp parallel for schedule(dynamic, 1)
+#pragma omp parallel for schedule(dynamic, 1) if (!ORC_INNER_PAR(n))
 #endif
   for (int64_t g = 0; g < S; ++g) {
     const int inst = (int)(g / n_traj);

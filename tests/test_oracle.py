@@ -246,3 +246,24 @@ def test_fused_cpu_restatement_matches_gate_oracle(pkg, L, T, pol, state, toff, 
     b = c_oracle.autocorr_fused(spec, 3, seed=5)
     assert np.abs(a["fwd"] - b["fwd"]).max() < 1e-12
     assert np.abs(a["echo"] - b["echo"]).max() < 1e-12
+
+
+def test_large_state_sweep_thread_independent(pkg):
+    """States of 2^22 amplitudes and more are swept by all threads, one
+    trajectory at a time (the L=28 parity runs, test_gpu_l28_oracle.py): the
+    gates are element-wise, so one thread and four give the same trajectory;
+    only measure_z's partial sums over 4M amplitudes are grouped differently (1e-11)."""
+    L = 22
+    rng = np.random.default_rng(5)
+    hs, phis = random_disorder(rng, L, 1)
+    spec = pkg.SweepSpec(L=L, T=3, hs=hs, phis=phis, g=0.93, noise_prob=0.05,
+                         polarization="circular_left", initial_state="neel")
+    one = c_oracle.autocorr(spec, 2, seed=9, want_zsite=True, n_threads=1)
+    four = c_oracle.autocorr(spec, 2, seed=9, want_zsite=True, n_threads=4)
+    for k in one:
+        assert np.abs(one[k] - four[k]).max() < 1e-11, k
+    # and the same trajectory as the small-state (per-trajectory threaded)
+    # path's arithmetic: the fused restatement agrees to 1e-10
+    fused = c_oracle.autocorr_fused(spec, 2, seed=9, n_threads=4)
+    for k in ("fwd", "echo"):
+        assert np.abs(one[k] - fused[k]).max() < 1e-10, k
