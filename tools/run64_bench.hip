@@ -9,6 +9,8 @@
 //   R128  lanes 0, 1, 2, 6, 7, 14 (128-B runs), id 3, 4, 5, 15..19
 //   R256  lanes 0..3, 6, 7 (256-B runs), id 4, 5, 14..19
 //   RC    lanes 0..5, waves 6, 7 (contiguous tiles), id 12..19
+//   R16   lanes 4..9, waves 10, 11, registers 12..15, id 0..3, 16..19: no run at
+//         all (16-B pieces; each 128-B line is read by 8 tiles, consecutive blocks)
 // Prints time and GB/s per pattern; run under rocprofv3 --pmc FETCH_SIZE to
 // compare the counter with the bytes read (16 GiB per launch).
 // build: hipcc --offload-arch=gfx950 -O3 tools/run64_bench.hip -o tools/run64_bench
@@ -49,6 +51,11 @@ template <>
 struct Pat<2> {
   static constexpr int lane[6] = {0, 1, 2, 3, 6, 7}, wave[2] = {12, 13}, reg[4] = {8, 9, 10, 11};
   static constexpr int id[8] = {4, 5, 14, 15, 16, 17, 18, 19};
+};
+template <>
+struct Pat<4> {  // R16: a 12-site window without column bits (16-B pieces)
+  static constexpr int lane[6] = {4, 5, 6, 7, 8, 9}, wave[2] = {10, 11}, reg[4] = {12, 13, 14, 15};
+  static constexpr int id[8] = {0, 1, 2, 3, 16, 17, 18, 19};
 };
 template <>
 struct Pat<3> {
@@ -95,11 +102,12 @@ int main() {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const dim3 grid(8 * 256, kStates / 8), block(256);
-  const char* names[8] = {"R64  nt (lcw2 load: 64-B runs)", "R128 nt (128-B runs)",
-                          "R256 nt (256-B runs)", "RC   nt (contiguous tiles)",
-                          "R64  temporal", "R128 temporal", "R256 temporal", "RC   temporal"};
+  const char* names[10] = {"R64  nt (lcw2 load: 64-B runs)", "R128 nt (128-B runs)",
+                           "R256 nt (256-B runs)", "RC   nt (contiguous tiles)",
+                           "R64  temporal", "R128 temporal", "R256 temporal", "RC   temporal",
+                           "R16  nt (16-B pieces)", "R16  temporal"};
   for (int rep = 0; rep < 2; ++rep) {
-    for (int p = 0; p < 8; ++p) {
+    for (int p = 0; p < 10; ++p) {
       auto launch = [&]() {
         if (p == 0) hipLaunchKernelGGL((k_read<0, true>), grid, block, 0, 0, s, out);
         if (p == 1) hipLaunchKernelGGL((k_read<1, true>), grid, block, 0, 0, s, out);
@@ -109,6 +117,8 @@ int main() {
         if (p == 5) hipLaunchKernelGGL((k_read<1, false>), grid, block, 0, 0, s, out);
         if (p == 6) hipLaunchKernelGGL((k_read<2, false>), grid, block, 0, 0, s, out);
         if (p == 7) hipLaunchKernelGGL((k_read<3, false>), grid, block, 0, 0, s, out);
+        if (p == 8) hipLaunchKernelGGL((k_read<4, true>), grid, block, 0, 0, s, out);
+        if (p == 9) hipLaunchKernelGGL((k_read<4, false>), grid, block, 0, 0, s, out);
       };
       launch();
       CHECK(hipDeviceSynchronize());
