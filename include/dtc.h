@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 9
+#define DTC_ABI_VERSION 10
 
 /* error codes */
 #define DTC_OK 0
@@ -318,9 +318,10 @@ int dtc_kernel_stats(dtc_ctx* ctx, int32_t kind, int64_t* launches,
 int dtc_reset_stats(dtc_ctx* ctx);
 /* Light-cone ends launched since dtc_open, by kernel: counts[0] the 8-site
  * window (dtc_lc_final*), [1] the 10-site window's generic kernel
- * (dtc_lcw_final), [2] its three-re-layout C2 form (dtc_lcw2_final).
+ * (dtc_lcw_final), [2] its three-re-layout C2 form (dtc_lcw2_final), [3] the
+ * 12-site window (dtc_lcw3_final, six passes merged; ABI 10).
  * Independent of profiling; lets tests assert which kernel a sweep ran. */
-int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [3] */);
+int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
 
 /* Device properties for reports. */
 int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
 KERNEL_KINDS = 6  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass,
                   # virtual-rank exchange
-ABI_VERSION = 9  # DTC_ABI_VERSION of include/dtc.h this binding matches
+ABI_VERSION = 10  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (

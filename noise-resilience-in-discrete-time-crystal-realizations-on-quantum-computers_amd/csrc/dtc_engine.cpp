@@ -106,6 +106,7 @@ struct dtc_ctx {
   int lc_split = 1;          // DTC_LC_SPLIT
   int lc_tpb = 0;            // DTC_LC_TPB (0 = default)
   bool lc_wide = true;       // DTC_NO_LCW unset: five-pass (10-site) light-cone ends
+  bool lc_wide3 = true;      // DTC_NO_LCW3 unset: six-pass (12-site) ends where they fit
   HostBuf host_f, host_e;    // pinned result staging (autocorr / energy)
   uint64_t tables_key = 0;   // upload_tables: the problem whose tables are in place
   bool tables_valid = false;
@@ -118,7 +119,7 @@ struct dtc_ctx {
   bool verbose = false;      // DTC_VERBOSE
   int prefix_octet = 0;      // layout the prefix states were built in
   int64_t st_n[DTC_KERNEL_KINDS] = {};
-  int64_t lc_launches[3] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
+  int64_t lc_launches[4] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
   bool dual = true;  // DTC_NO_DUAL: echo chains start with a pass of their own
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
@@ -372,10 +373,22 @@ struct PassSpec {
   // bit 10 l + k - 2 = tile bit k kicked in layer l
   int lc_wide = 0;
   int8_t lc_gb[dtc::kTileBits] = {};
+  // the 12-site form (lc_wide = 2, lc_merge_wide7): tile bit k = global bit
+  // j-5+k, bit 12 l + k of the 84-bit mask lc_mask | lc_mask2 << 64
+  uint64_t lc_mask2 = 0;
 };
 
 // the tile bits a light-cone pass kicks in layer l (nonzero: the layer runs)
 uint64_t lc_layer_bits(const PassSpec& ps, int l) {
+  if (ps.lc_wide == 2) {
+    uint64_t m = 0;
+    for (int k = 0; k < dtc::kTileBits; ++k) {
+      const int bit = 12 * l + k;
+      const uint64_t on = bit < 64 ? (ps.lc_mask >> bit) & 1ull : (ps.lc_mask2 >> (bit - 64)) & 1ull;
+      m |= on << k;
+    }
+    return m;
+  }
   return ps.lc_wide ? (ps.lc_mask >> (10 * l)) & 0x3FFull
                     : (ps.lc_mask >> (dtc::kLcSites * l)) & 0xFFull;
 }
@@ -526,6 +539,7 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
   pk.lc_layers = ps.lc_layers;
   for (int l = 0; l < dtc::kLcMaxLayers; ++l) pk.lc[l] = ps.lc[l];
   pk.lc_mask = ps.lc_mask;
+  pk.lc_mask2 = ps.lc_mask2;
   pk.lc_wide = ps.lc_wide;
   for (int k = 0; k < dtc::kTileBits; ++k) pk.lc_gb[k] = ps.lc_gb[k];
   pk.kind = pass_kind(rc, ps, pass_shape(ps));
@@ -625,6 +639,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.no_store = no_store;
   A.lc_layers = ps.lc_layers;
   A.lc_mask = ps.lc_mask;
+  A.lc_mask2 = ps.lc_mask2;
   A.lc_diag = (const double2*)ctx->lc_diag.p;
   A.lc_wide = ps.lc_wide;
   for (int k = 0; k < dtc::kTileBits; ++k) A.lc_gb[k] = ps.lc_gb[k];
@@ -651,7 +666,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   } else {
     DTC_HIP(dtc::launch_pass(A, batch, shape, kind, ctx->stream, &lc_variant));
   }
-  if (lc_variant >= 0 && lc_variant < 3) ++ctx->lc_launches[lc_variant];
+  if (lc_variant >= 0 && lc_variant < 4) ++ctx->lc_launches[lc_variant];
   if (ctx->prof) {
     DTC_HIP(hipEventRecord(e1, ctx->stream));
     // algorithmic bytes: a read and a store per amplitude, or one of them
@@ -910,6 +925,25 @@ void build_cone_tables(int L, int j, int n_inst, const double* h, const double* 
         o[2 * e + 1] = std::sin(-0.5 * ang);
       }
     }
+    // r = 6 and r = 3 split at j (dtc_lcw3_final; j - 6 >= 0 and j + 6 < L,
+    // the only geometry that kernel runs): bits j-6 .. j (fields j-5 .. j,
+    // bonds from j-6) and j .. j+6 (fields j+1 .. j+5, bonds up to j+6); bits
+    // j-3 .. j and j .. j+3 likewise
+    if (j - 6 >= 0 && j + 6 <= L - 1) {
+      for (int part = 0; part < 4; ++part) {
+        const int off = part == 0 ? dtc::kLcTab6a : part == 1 ? dtc::kLcTab6b
+                      : part == 2 ? dtc::kLcTab3a : dtc::kLcTab3b;
+        const int r = part < 2 ? 6 : 3;
+        double* o = out.data() + ((size_t)in * dtc::kLcTab + off) * 2;
+        for (int v = 0; v < (1 << (r + 1)); ++v) {
+          const double ang = (part % 2 == 0)
+                                 ? diag_angle(L, hh, pp, j - r + 1, j + 1, j - r, j, j - r, v)
+                                 : diag_angle(L, hh, pp, j + 1, j + r, j, j + r, j, v);
+          o[2 * v] = std::cos(-0.5 * ang);
+          o[2 * v + 1] = std::sin(-0.5 * ang);
+        }
+      }
+    }
     // r = 4 split at j (dtc_lcw2_final): the product of the two is the r = 4
     // table (dtc_kernels.h kLcTab4a / kLcTab4b; j - 4 >= 0 and j + 4 < L, the
     // only geometry that kernel runs)
@@ -1144,15 +1178,66 @@ bool lc_merge_wide(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, 
   return true;
 }
 
+// The 12-site light-cone end (dtc_lcw3_final): the chain's last six passes
+// as seven layers r = 6 .. 0 on the window j-5 .. j+6, tile bit k = global
+// bit j-5+k (no column bits).  The kernel runs a fixed program: layer l may
+// kick only sites of its cone that the program visits (l0: j+2 .. j+6 -- the
+// C2 chains' first layer is group B's pre-kick; l1: j-5 .. j+5; then the
+// cones of radius 4 .. 0); a site the chain leaves unkicked gets the identity
+// record.  False leaves the chain to lc_merge_wide.
+bool lc_merge_wide7(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j) {
+  const Plan& pl = rc.pl;
+  const int L = pl.L;
+  if ((int)(sched.size() - chain0) < 6) return false;
+  if (j - 6 < 0 || j + 6 > L - 1 || pl.L_eff != L || pl.L_eff > 32) return false;
+  std::vector<KickDesc> desc;
+  std::vector<uint64_t> sites;
+  if (!lc_layers_of(rc, sched, 6, desc, sites) || (int)desc.size() != dtc::kLcw3Layers) return false;
+  auto span = [&](int a, int b) {  // sites j+a .. j+b
+    uint64_t m = 0;
+    for (int i = j + a; i <= j + b; ++i) m |= 1ull << i;
+    return m;
+  };
+  const uint64_t prog[dtc::kLcw3Layers] = {span(2, 6), span(-5, 5), span(-4, 4), span(-3, 3),
+                                           span(-2, 2), span(-1, 1), span(0, 0)};
+  for (int l = 0; l < dtc::kLcw3Layers; ++l) {
+    sites[l] &= cone_sites(L, j, dtc::kLcw3Layers - 1 - l);
+    if (sites[l] & ~prog[l]) return false;
+  }
+  PassSpec lc{sched.back().ps.group, no_kick(), no_kick(), dtc::kDiagConj, sched.back().ps.d_index};
+  lc.lc_w0 = j - 5;  // (marks the light-cone pass; the tile is lc_gb)
+  lc.lc_wide = 2;
+  lc.lc_layers = dtc::kLcw3Layers;
+  for (int k = 0; k < dtc::kTileBits; ++k) lc.lc_gb[k] = (int8_t)(j - 5 + k);
+  for (int l = 0; l < dtc::kLcw3Layers; ++l) {
+    lc.lc[l] = desc[l];
+    for (int k = 0; k < dtc::kTileBits; ++k)
+      if ((sites[l] >> (j - 5 + k)) & 1ull) {
+        const int bit = 12 * l + k;
+        if (bit < 64) lc.lc_mask |= 1ull << bit;
+        else lc.lc_mask2 |= 1ull << (bit - 64);
+      }
+  }
+  const int kind = pass_kind(rc, lc, dtc::kShapeLC);
+  if (kind != dtc::kKindRX && kind != dtc::kKindRY) return false;
+  const Launch first = sched[sched.size() - 6];
+  sched.resize(sched.size() - 6 + 1);
+  sched.back() = Launch{lc, first.src, first.dst, dtc::kMeasProbe, 1, 2, nullptr, first.meas_stride};
+  return true;
+}
+
 // Light-cone end of the echo chain sched[chain0 ..) measuring Z_j: replace
-// its last k passes by one kShapeLC pass -- five (lc_merge_wide, when enabled
-// and it fits), else k = 4 .. 2 (the first that fits) over an 8-site window.
+// its last k passes by one kShapeLC pass -- six (lc_merge_wide7) or five
+// (lc_merge_wide), when enabled and they fit, else k = 4 .. 2 (the first that
+// fits) over an 8-site window.
 // Layer l of M (r = M - 1 - l diagonals before the probe) only matters on
 // sites j-r .. j+r, and the layers' remaining sites must fit the window
 // w0 .. w0+7 (4 <= w0 <= L - 8: clear of tile bits 0..3).
-void lc_merge(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j, bool wide) {
+void lc_merge(const RunCfg& rc, std::vector<Launch>& sched, size_t chain0, int j, bool wide,
+              bool wide3) {
   const Plan& pl = rc.pl;
   const int L = pl.L;
+  if (wide3 && lc_merge_wide7(rc, sched, chain0, j)) return;
   if (wide && lc_merge_wide(rc, sched, chain0, j)) return;
   const int n_chain = (int)(sched.size() - chain0);
   for (int k = std::min(4, n_chain); k >= 2; --k) {
@@ -1223,6 +1308,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   // with the full passes, each form on its own engine)
   c->lightcone = std::getenv("DTC_NO_LIGHTCONE") == nullptr;
   c->lc_wide = std::getenv("DTC_NO_LCW") == nullptr;
+  c->lc_wide3 = c->lc_wide && std::getenv("DTC_NO_LCW3") == nullptr;
   c->dual = std::getenv("DTC_NO_DUAL") == nullptr;
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1304,7 +1390,7 @@ int dtc_reset_stats(dtc_ctx* ctx) {
 
 int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts) {
   if (!ctx || !counts) return fail(DTC_EINVAL, "null ctx / counts");
-  for (int k = 0; k < 3; ++k) counts[k] = ctx->lc_launches[k];
+  for (int k = 0; k < 4; ++k) counts[k] = ctx->lc_launches[k];
   return DTC_OK;
 }
 
@@ -1591,7 +1677,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         // of the kicks left: their layers, restricted to the cone, with D*
         // between them, then the probe.
         if (!rc.device && lc_enabled && sched.size() - chain0 >= 2)
-          lc_merge(rc, sched, chain0, pr->probe_site, ctx->lc_wide);
+          lc_merge(rc, sched, chain0, pr->probe_site, ctx->lc_wide, ctx->lc_wide3);
         sched.back().meas_mode = dtc::kMeasProbe;
         sched.back().meas_out = (double*)ctx->vals_e.p + (size_t)t * 2;
         // the echo state is only measured: the chain's last pass reads its

@@ -95,7 +95,15 @@ static constexpr int kLcTab5b = kLcTab4 + 64;
 // kernel's tables fit four workgroups per CU.
 static constexpr int kLcTab4a = kLcTab4 + 128;
 static constexpr int kLcTab4b = kLcTab4 + 160;
-static constexpr int kLcTab = kLcTab4 + 192;  // per-instance stride of PassArgs::lc_diag
+// The 12-site pass (dtc_lcw3_final) adds r = 6 split at j (bits j-6 .. j:
+// fields j-5 .. j, bonds (j-6, j-5) .. (j-1, j); bits j .. j+6: fields j+1 ..
+// j+5, bonds (j, j+1) .. (j+5, j+6)) and r = 3 split at j (bits j-3 .. j and
+// j .. j+3), natural order.
+static constexpr int kLcTab6a = kLcTab4 + 192;
+static constexpr int kLcTab6b = kLcTab4 + 320;
+static constexpr int kLcTab3a = kLcTab4 + 448;
+static constexpr int kLcTab3b = kLcTab4 + 464;
+static constexpr int kLcTab = kLcTab4 + 480;  // per-instance stride of PassArgs::lc_diag
 // kShapeLC with lc_wide: six kick layers over a 10-site window (one more
 // pass of the echo chain merged).  Tile bits 0, 1 = global bits 0, 1 (64-B
 // runs), tile bits 2 .. 11 = window sites lc_gb[2 .. 11] (host-chosen: nibble
@@ -108,7 +116,16 @@ static constexpr int kLcTab = kLcTab4 + 192;  // per-instance stride of PassArgs
 static constexpr int kLcwLayers = 6;
 static constexpr int kLcwG2 = 12 * kLcwLayers;
 static constexpr int kLcwMask = kLcwG2 + 1;
-static constexpr int kLcMaxLayers = kLcwLayers;
+// kShapeLC with lc_wide = 2 (dtc_lcw3_final): seven layers over a 12-site
+// window, tile bit k = global bit j-5+k (no column bits), one more pass of
+// the echo chain merged; kick of (layer l, tile bit k) when bit 12 l + k of
+// the 84-bit mask (lc_mask: bits 0..63, lc_mask2: 64..83) is set.  Records:
+// f^ of (l, k) at 12 l + k, kLcw3G2: prod w^2, kLcw3Mask + l: the frame's X
+// mask after layer l in global bit positions.
+static constexpr int kLcw3Layers = 7;
+static constexpr int kLcw3G2 = 12 * kLcw3Layers;
+static constexpr int kLcw3Mask = kLcw3G2 + 1;
+static constexpr int kLcMaxLayers = kLcw3Layers;
 // Matrix family of every kick in a pass (chosen by the host from the kick
 // table): Pauli x RX(theta) = i^k [[a, ib], [ic, d]], Pauli x RY(theta) =
 // i^k [[a, b], [c, d]] (4 flops per amplitude), anything else general (8).
@@ -163,6 +180,7 @@ struct PassKick {
   uint64_t lc_mask;     // bit 4 + b); Pauli-frame records (kLcCoefs ..)
   int lc_wide;          // the 10-site form: lc_mask bit 10 l + k - 2 = tile bit k of
   int8_t lc_gb[kTileBits];  // layer l, tile bit k = global bit lc_gb[k] (kLcw* records)
+  uint64_t lc_mask2;    // lc_wide = 2: bits 64..83 of the 12-site form's mask
 };
 
 struct PrepArgs {
@@ -228,7 +246,8 @@ struct PassArgs {
   uint64_t lc_mask;
   const double2* lc_diag;  // kShapeLC: cone diagonals, [n_inst][kLcTab]
   int lc_wide;             // kShapeLC: the 10-site form (dtc_lcw_final), tile bit k =
-  int8_t lc_gb[kTileBits]; // global bit lc_gb[k]
+  int8_t lc_gb[kTileBits]; // global bit lc_gb[k]; 2: the 12-site form (dtc_lcw3_final)
+  uint64_t lc_mask2;       // lc_wide = 2: bits 64..83 of its mask
   int zx_reg, zx_lane;      // kMeasEnergy: the bond between register bit zx_reg and lane
                            // bit zx_lane of the measured layout (-1: none), host-computed
   double* partial;         // [B][n_tiles][n_obs]
@@ -278,7 +297,7 @@ hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStr
                        int* lc_variant = nullptr);
 
 // kShapeLC passes (dtc_lightcone.hip), from launch_pass with its grid
-enum LcVariant { kLcVariant8 = 0, kLcVariantWide = 1, kLcVariantWide2 = 2 };
+enum LcVariant { kLcVariant8 = 0, kLcVariantWide = 1, kLcVariantWide2 = 2, kLcVariantWide3 = 3 };
 hipError_t launch_lightcone(const PassArgs& a, dim3 grid, int kind, hipStream_t stream,
                             int* variant);
 

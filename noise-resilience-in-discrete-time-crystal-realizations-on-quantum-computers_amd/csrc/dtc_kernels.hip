@@ -245,6 +245,45 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   const int64_t gstate = P.batch_start + b;
   const uint64_t traj = (uint64_t)(P.traj_offset + (gstate % P.n_traj));
   KickRec* out = P.out + id * kRecPerState;
+  if (pk.lc_layers > 0 && pk.lc_wide == 2) {
+    // 12-site light-cone pass (dtc_kernels.h, kLcw3*): the Pauli frame over
+    // all twelve tile bits, seven layers, mask bit 12 l + k in lc_mask /
+    // lc_mask2; the X masks in global bit positions
+    double* od = (double*)out;
+    long long* oi = (long long*)out;
+    int fz = 0, fx = 0;  // per tile bit
+    double g2 = 1.0;
+    for (int l = 0; l < kLcw3Layers; ++l) {
+      for (int k = 0; k < kTileBits; ++k) {
+        const int bit = 12 * l + k;
+        const bool on = bit < 64 ? ((pk.lc_mask >> bit) & 1ull) : ((pk.lc_mask2 >> (bit - 64)) & 1ull);
+        double fh = 0.0;
+        if (l < pk.lc_layers && on) {
+          const int lsite = pk.lc_gb[k];
+          double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0),
+                          make_double2(0.0, 0.0), make_double2(1.0, 0.0)};
+          if (lsite < P.L_real)
+            build_site_kick(P, pk.lc[l], P.site_of ? P.site_of[lsite] : lsite, traj, m);
+          SiteMat sm;
+          canonicalise(pk.kind, m, sm);
+          const int form_b = sm.var >> 1, neg = sm.var & 1;
+          const double ft = form_b ? -sm.coef : sm.coef;
+          const int flip = ((pk.kind == kKindRX ? fz : (fz ^ fx)) >> k) & 1;
+          fh = flip ? -ft : ft;
+          fz ^= (pk.kind == kKindRX ? neg : (neg ^ form_b)) << k;
+          fx ^= form_b << k;
+          g2 *= sm.scale * sm.scale;
+        }
+        od[12 * l + k] = fh;
+      }
+      long long mg = 0;
+      for (int k = 0; k < kTileBits; ++k)
+        if ((fx >> k) & 1) mg |= 1ll << pk.lc_gb[k];
+      oi[kLcw3Mask + l] = mg;
+    }
+    od[kLcw3G2] = g2;
+    return;
+  }
   if (pk.lc_layers > 0 && pk.lc_wide) {
     // 10-site light-cone pass: the same Pauli frame over tile bits 2 .. 11
     // (dtc_kernels.h, kLcw*); the X masks in global bit positions

@@ -857,11 +857,352 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
   }
 }
 
+// ---- the 12-site light-cone end, C2 form (dtc_lcw3_final) ------------------
+// One more pass of the echo chain merged: seven layers l0 .. l6 (cone radius
+// 6 .. 0) over the window j-5 .. j+6 (sites m5 .. p6; the C2 chains' first
+// layer is group B's pre-kick, p2 .. p6), tile bit k = global bit j-5+k.  No
+// column bits: the tile reads 16-B pieces, each 128-B line shared by eight
+// consecutive tiles of the same XCD (ordinary loads: L2 serves the partners,
+// tools/run64_bench.hip R16: 3.1 TB/s at x1.00 of the bytes, the pass needs
+// less).  Program (register sites, swaps into lane bits 4 / 5):
+//   X1  p3 p4 p5 p6 | l0: p3 p4 p5 p6, swap p2 in, p2 | D6 | l1: p3 p4 p5 p2,
+//                     swap m5 in, m5
+//   X2  m4 m3 m2 m1 | l1: m4 m3 m2 m1, swap z0 p1 in, z0 p1 | D5 | l2: z0 p1
+//                     m2 m1, swap m4 m3 back, m4 m3
+//   X3  p2 p3 p4 m3 | l2: p2 p3 p4 | D4 | l3: p2 p3 m3
+//   X4  m2 m1 z0 p1 | l3: m2 m1 z0 p1 | D3 | l4: m2 m1 z0 p1, swap p2 in, p2 |
+//                     D2 | l5: m1 z0 p1 | D1 | l6: z0 | probe
+// 41 site kicks, three LDS re-layouts, seven row swaps.  Re-layout slots are
+// the tile index mapped by an invertible GF(2) matrix (lcw3::cv: 4096 slots,
+// the thread's base XOR a compile-time register part): the low five bits of
+// the lane sites' vectors are independent in every layout written (lanes 0..3)
+// and read (lanes 0..4), so the accesses are conflict-free.  The cone
+// diagonals r = 6, 5, 4, 3 are split at j (two tables each, 456 entries with
+// r = 2 and 1; the r = 6 left table staged for the workgroup's bit j-6 only):
+// 40.1 KB of LDS, four workgroups per CU.
+namespace lcw3 {
+enum : int { m5 = 0, m4, m3, m2, m1, z0, p1, p2, p3, p4, p5, p6, kNSite };
+__host__ __device__ constexpr int off_of(int s) { return s - z0; }
+__host__ __device__ constexpr int cv(int s) {
+  return s == m4 ? 1 : s == m3 ? 2 : s == m2 ? 4 : s == m1 ? 8 : s == z0 ? 16
+       : s == p3 ? 32 | 1 : s == p4 ? 64 | 2 : s == p1 ? 128 | 2 : s == p5 ? 256 | 4
+       : s == p6 ? 512 | 8 : s == p2 ? 1024 | 16 : 2048;
+}
+// layouts: positions 0..3 registers, 4..9 lane bits 0..5, 10..11 wave bits
+enum : int { kX1 = 0, kX1e, kX1f, kX2, kX2s, kX3, kX4, kX4e };
+__host__ __device__ constexpr int lay_site(int li, int pos) {
+  constexpr int tab[8][12] = {
+      {p3, p4, p5, p6, m4, m3, m2, m1, p2, m5, z0, p1},   // X1 (load)
+      {p3, p4, p5, p2, m4, m3, m2, m1, p6, m5, z0, p1},   // X1e: R3 <-> lane 4
+      {m5, p4, p5, p2, m4, m3, m2, m1, p6, p3, z0, p1},   // X1f: R0 <-> lane 5
+      {m4, m3, m2, m1, p3, p4, p5, p6, z0, p1, m5, p2},   // X2
+      {z0, p1, m2, m1, p3, p4, p5, p6, m4, m3, m5, p2},   // X2s: R0 <-> lane 4, R1 <-> lane 5
+      {p2, p3, p4, m3, m4, p1, m2, m1, z0, m5, p5, p6},   // X3
+      {m2, m1, z0, p1, m4, m3, p5, p6, p2, m5, p3, p4},   // X4
+      {p2, m1, z0, p1, m4, m3, p5, p6, m2, m5, p3, p4}};  // X4e: R0 <-> lane 4
+  return tab[li][pos];
+}
+__host__ __device__ constexpr int reg_slot(int li, int r) {
+  return ((r & 1) ? cv(lay_site(li, 0)) : 0) ^ ((r & 2) ? cv(lay_site(li, 1)) : 0) ^
+         ((r & 4) ? cv(lay_site(li, 2)) : 0) ^ ((r & 8) ? cv(lay_site(li, 3)) : 0);
+}
+template <int LI>
+__device__ __forceinline__ int slot_base(int t) {
+  int b = 0;
+#pragma unroll
+  for (int p = 4; p < 12; ++p) b ^= ((t >> (p - 4)) & 1) * cv(lay_site(LI, p));
+  return b;
+}
+// cone tables in LDS (double2 entries), natural index order from bit lo
+enum : int { kT6a = 0, kT6b, kT5a, kT5b, kT4a, kT4b, kT3a, kT3b, kT2, kT1, kNTab };
+__host__ __device__ constexpr int tab_off(int k) {
+  return k == kT6a ? 0 : k == kT6b ? 64 : k == kT5a ? 192 : k == kT5b ? 256 : k == kT4a ? 320
+       : k == kT4b ? 352 : k == kT3a ? 384 : k == kT3b ? 400 : k == kT2 ? 416 : 448;
+}
+static constexpr int kTabEntries = 456;
+__host__ __device__ constexpr int tab_bits(int k) {
+  return k == kT6a ? 6 : k == kT6b ? 7 : (k == kT5a || k == kT5b) ? 6 : (k == kT4a || k == kT4b) ? 5
+       : (k == kT3a || k == kT3b) ? 4 : k == kT2 ? 5 : 3;
+}
+__host__ __device__ constexpr int tab_lo(int k) {  // offset from j of index bit 0
+  return k == kT6a ? -5 : k == kT5a ? -5 : k == kT4a ? -4 : k == kT3a ? -3 : k == kT2 ? -2
+       : k == kT1 ? -1 : 0;
+}
+__host__ __device__ constexpr int tab_layer(int k) {
+  return (k == kT6a || k == kT6b) ? 0 : (k == kT5a || k == kT5b) ? 1 : (k == kT4a || k == kT4b) ? 2
+       : (k == kT3a || k == kT3b) ? 3 : k == kT2 ? 4 : 5;
+}
+__host__ __device__ constexpr int tab_src(int k) {
+  return k == kT6a ? kLcTab6a : k == kT6b ? kLcTab6b : k == kT5a ? kLcTab5a : k == kT5b ? kLcTab5b
+       : k == kT4a ? kLcTab4a : k == kT4b ? kLcTab4b : k == kT3a ? kLcTab3a : k == kT3b ? kLcTab3b
+       : lc_tab_off(k == kT2 ? 2 : 1);
+}
+__host__ __device__ constexpr int tab_wt(int k, int s) {
+  const int d = off_of(s) - tab_lo(k);
+  return (d < 0 || d >= tab_bits(k)) ? 0 : 1 << d;
+}
+template <int LI, int K>
+__device__ __forceinline__ int tab_reg(int r) {
+  return ((r & 1) ? tab_wt(K, lay_site(LI, 0)) : 0) + ((r & 2) ? tab_wt(K, lay_site(LI, 1)) : 0) +
+         ((r & 4) ? tab_wt(K, lay_site(LI, 2)) : 0) + ((r & 8) ? tab_wt(K, lay_site(LI, 3)) : 0);
+}
+template <int LI, int K>
+__device__ __forceinline__ int tab_base(int t) {
+  int b = 0;
+#pragma unroll
+  for (int p = 4; p < 12; ++p) b += ((t >> (p - 4)) & 1) * tab_wt(K, lay_site(LI, p));
+  return b;
+}
+}  // namespace lcw3
+
+template <int KIND>
+__global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
+  static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
+  using namespace lcw3;
+  __shared__ double s_x[kTile];
+  __shared__ double2 s_tab[kTabEntries];
+  __shared__ double s_red[kThreads / 64][2];
+  const int t = threadIdx.x;
+  const int64_t n_tiles = (int64_t)1 << (A.L_eff - kTileBits);
+  const int og = A.octet_bits;
+  const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
+  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  if (og && b >= A.batch) return;
+  const int inst = (int)((A.batch_start + b) / A.n_traj);
+  const int j = A.probe;
+  RecRegs R;
+  {
+    const int lane = t & 63;
+    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
+    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+    if (4 * lane < kLcw3Mask + kLcw3Layers) {  // the records: lanes 0 .. 22
+      r0 = rp[0];
+      r1 = rp[1];
+    }
+    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
+  }
+  // global bit of each window site; the tile's base: its id in bits
+  // 0 .. j-6 and j+7 .. (the host checks j >= 6: bit j-6 is an id bit)
+  auto gpos = [&](int s) { return j + off_of(s); };
+  const uint32_t tbase = ((uint32_t)tile & ((1u << (j - 5)) - 1u)) |
+                         (((uint32_t)tile >> (j - 5)) << (j + 7));
+  const int b6 = (int)((tbase >> (j - 6)) & 1u);  // table 6a's bit j-6
+  double2 v[kRegs];
+  auto xch = [&](auto from_tag, auto to_tag) {
+    constexpr int F = decltype(from_tag)::value, T = decltype(to_tag)::value;
+    int bf = slot_base<F>(t), bt = slot_base<T>(t);
+    asm volatile("" : "+v"(bf), "+v"(bt));
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) s_x[bf ^ reg_slot(F, r)] = v[r].x;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r].x = s_x[bt ^ reg_slot(T, r)];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) s_x[bf ^ reg_slot(F, r)] = v[r].y;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r].y = s_x[bt ^ reg_slot(T, r)];
+  };
+  auto kick = [&](auto q_tag, auto l_tag, auto s_tag) {
+    constexpr int Q = decltype(q_tag)::value, l = decltype(l_tag)::value, S = decltype(s_tag)::value;
+    layer_f<KIND, 0, Q>(v, R.d(0, 12 * l + S));
+  };
+  // v[r] *= TA[reg part] * TB[reg part] (two tables of one diagonal)
+  auto diag2 = [&](auto lay_tag, auto ka_tag, auto kb_tag) {
+    constexpr int LI = decltype(lay_tag)::value, KA = decltype(ka_tag)::value,
+                  KB = decltype(kb_tag)::value;
+    int ba = tab_base<LI, KA>(t), bb = tab_base<LI, KB>(t);
+    asm volatile("" : "+v"(ba), "+v"(bb));
+    const double2* ta = s_tab + tab_off(KA) + ba;
+    const double2* tb = s_tab + tab_off(KB) + bb;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r)
+      v[r] = cmul(v[r], cmul(ta[tab_reg<LI, KA>(r)], tb[tab_reg<LI, KB>(r)]));
+  };
+  auto diag1 = [&](auto lay_tag, auto k_tag) {
+    constexpr int LI = decltype(lay_tag)::value, K = decltype(k_tag)::value;
+    int base = tab_base<LI, K>(t);
+    asm volatile("" : "+v"(base));
+    const double2* tab = s_tab + tab_off(K) + base;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], tab[tab_reg<LI, K>(r)]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+  using C3 = std::integral_constant<int, 3>;
+  using C4 = std::integral_constant<int, 4>;
+  using C5 = std::integral_constant<int, 5>;
+  using C6 = std::integral_constant<int, 6>;
+#define LCW3_S(s) std::integral_constant<int, s>{}
+#define LCW3_L(x) std::integral_constant<int, x>{}
+  // the tile in layout X1 (ordinary loads: 16-B pieces, note above dtc_lcw2_final)
+  {
+    uint32_t xl = 0;
+#pragma unroll
+    for (int p = 4; p < 12; ++p) xl |= (uint32_t)((t >> (p - 4)) & 1) << gpos(lay_site(kX1, p));
+    const int64_t vofs = octet_spread((int64_t)xl, og) << 4;
+    const char* src = (const char*)(A.src + state_base(b, A.state_len, og));
+    const int64_t sp0 = octet_spread((int64_t)tbase, og) << 4;
+    int64_t spq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) spq[q] = octet_spread((int64_t)1 << gpos(lay_site(kX1, q)), og) << 4;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      int64_t o = sp0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if ((r >> q) & 1) o += spq[q];
+      const d2v w = *(const d2v*)(src + o + vofs);
+      v[r] = make_double2(w.x, w.y);
+    }
+  }
+  // the cone-table entries this thread stages (e = t, t + 256 of the 456):
+  // loaded behind the tile, staged after the first layer
+  const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
+  auto tab_of = [](int e) {
+    return e >= tab_off(kT1) ? kT1 : e >= tab_off(kT2) ? kT2 : e >= tab_off(kT3b) ? kT3b
+         : e >= tab_off(kT3a) ? kT3a : e >= tab_off(kT4b) ? kT4b : e >= tab_off(kT4a) ? kT4a
+         : e >= tab_off(kT5b) ? kT5b : e >= tab_off(kT5a) ? kT5a : e >= tab_off(kT6b) ? kT6b : kT6a;
+  };
+  // entry i of table k in the instance's tables (6a: the workgroup's bit j-6
+  // is index bit 0 there; 5a is stored lc_pos5a-swizzled)
+  auto src_index = [&](int k, int i) {
+    return tab_src(k) + (k == kT6a ? ((i << 1) | b6) : k == kT5a ? lc_pos5a(i) : i);
+  };
+  const int e1 = t + kThreads;
+  const int k0 = tab_of(t), k1 = e1 < kTabEntries ? tab_of(e1) : kT1;
+  const int i0 = t - tab_off(k0), i1 = e1 - tab_off(k1);
+  const double2 tv0 = ct[src_index(k0, i0)];
+  double2 tv1 = make_double2(0.0, 0.0);
+  if (e1 < kTabEntries) tv1 = ct[src_index(k1, i1)];
+  // ---- X1: l0 on p3 p4 p5 p6, p2 (swapped in) ----
+  kick(C0{}, C0{}, LCW3_S(p3));
+  kick(C1{}, C0{}, LCW3_S(p4));
+  kick(C2{}, C0{}, LCW3_S(p5));
+  kick(C3{}, C0{}, LCW3_S(p6));
+  swap_reg_lane<3, 16>(v);  // register bit 3: p2 (lane bit 4: p6)
+  kick(C3{}, C0{}, LCW3_S(p2));
+  // stage the tables: entry i of table k at i ^ m_k, m_k the frame's X mask
+  // after the table's layer on the table's bits; conjugated for D*
+  {
+    const double cs = A.diag_conj ? -1.0 : 1.0;
+    const uint64_t mm0 = (uint64_t)R.bits(kLcw3Mask + 0), mm1 = (uint64_t)R.bits(kLcw3Mask + 1);
+    const uint64_t mm2 = (uint64_t)R.bits(kLcw3Mask + 2), mm3 = (uint64_t)R.bits(kLcw3Mask + 3);
+    const uint64_t mm4 = (uint64_t)R.bits(kLcw3Mask + 4), mm5 = (uint64_t)R.bits(kLcw3Mask + 5);
+    auto stage = [&](int k, int i, double2 tv) {
+      const int l = tab_layer(k);
+      const uint64_t m = l == 0 ? mm0 : l == 1 ? mm1 : l == 2 ? mm2 : l == 3 ? mm3 : l == 4 ? mm4 : mm5;
+      const int x = i ^ (int)((m >> (j + tab_lo(k))) & ((1u << tab_bits(k)) - 1u));
+      s_tab[tab_off(k) + x] = make_double2(tv.x, cs * tv.y);
+    };
+    stage(k0, i0, tv0);
+    if (e1 < kTabEntries) stage(k1, i1, tv1);
+  }
+  __syncthreads();  // the tables, before D6 (the first re-layout comes later)
+  // ---- D6 in X1e, l1 on p3 p4 p5 p2, m5 (swapped in) ----
+  diag2(LCW3_L(kX1e), LCW3_L(kT6a), LCW3_L(kT6b));
+  kick(C0{}, C1{}, LCW3_S(p3));
+  kick(C1{}, C1{}, LCW3_S(p4));
+  kick(C2{}, C1{}, LCW3_S(p5));
+  kick(C3{}, C1{}, LCW3_S(p2));
+  swap_reg_lane<0, 32>(v);  // register bit 0: m5 (lane bit 5: p3)
+  kick(C0{}, C1{}, LCW3_S(m5));
+  xch(LCW3_L(kX1f), LCW3_L(kX2));
+  // ---- X2: l1 on m4 m3 m2 m1, z0 p1 (swapped in), D5, l2 ----
+  kick(C0{}, C1{}, LCW3_S(m4));
+  kick(C1{}, C1{}, LCW3_S(m3));
+  kick(C2{}, C1{}, LCW3_S(m2));
+  kick(C3{}, C1{}, LCW3_S(m1));
+  swap_reg_lane<0, 16>(v);  // register bit 0: z0 (lane bit 4: m4)
+  swap_reg_lane<1, 32>(v);  // register bit 1: p1 (lane bit 5: m3)
+  kick(C0{}, C1{}, LCW3_S(z0));
+  kick(C1{}, C1{}, LCW3_S(p1));
+  diag2(LCW3_L(kX2s), LCW3_L(kT5a), LCW3_L(kT5b));
+  kick(C0{}, C2{}, LCW3_S(z0));
+  kick(C1{}, C2{}, LCW3_S(p1));
+  kick(C2{}, C2{}, LCW3_S(m2));
+  kick(C3{}, C2{}, LCW3_S(m1));
+  swap_reg_lane<0, 16>(v);  // back: register bit 0: m4
+  swap_reg_lane<1, 32>(v);  // register bit 1: m3
+  kick(C0{}, C2{}, LCW3_S(m4));
+  kick(C1{}, C2{}, LCW3_S(m3));
+  xch(LCW3_L(kX2), LCW3_L(kX3));
+  // ---- X3: l2 on p2 p3 p4, D4, l3 on p2 p3 m3 ----
+  kick(C0{}, C2{}, LCW3_S(p2));
+  kick(C1{}, C2{}, LCW3_S(p3));
+  kick(C2{}, C2{}, LCW3_S(p4));
+  diag2(LCW3_L(kX3), LCW3_L(kT4a), LCW3_L(kT4b));
+  kick(C0{}, C3{}, LCW3_S(p2));
+  kick(C1{}, C3{}, LCW3_S(p3));
+  kick(C3{}, C3{}, LCW3_S(m3));
+  xch(LCW3_L(kX3), LCW3_L(kX4));
+  // ---- X4: l3 on m2 m1 z0 p1, D3, l4, D2, l5, D1, l6 ----
+  kick(C0{}, C3{}, LCW3_S(m2));
+  kick(C1{}, C3{}, LCW3_S(m1));
+  kick(C2{}, C3{}, LCW3_S(z0));
+  kick(C3{}, C3{}, LCW3_S(p1));
+  diag2(LCW3_L(kX4), LCW3_L(kT3a), LCW3_L(kT3b));
+  kick(C0{}, C4{}, LCW3_S(m2));
+  kick(C1{}, C4{}, LCW3_S(m1));
+  kick(C2{}, C4{}, LCW3_S(z0));
+  kick(C3{}, C4{}, LCW3_S(p1));
+  swap_reg_lane<0, 16>(v);  // register bit 0: p2 (lane bit 4: m2)
+  kick(C0{}, C4{}, LCW3_S(p2));
+  diag1(LCW3_L(kX4e), LCW3_L(kT2));
+  kick(C1{}, C5{}, LCW3_S(m1));
+  kick(C2{}, C5{}, LCW3_S(z0));
+  kick(C3{}, C5{}, LCW3_S(p1));
+  diag1(LCW3_L(kX4e), LCW3_L(kT1));
+  kick(C2{}, C6{}, LCW3_S(z0));
+#undef LCW3_S
+#undef LCW3_L
+  // probe: j at register bit 2 of X4e; the frame's final X on j flips it
+  double ptot = 0.0, pz = 0.0;
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    const double p2v = fma(v[r].x, v[r].x, v[r].y * v[r].y);
+    ptot += p2v;
+    pz += ((r >> 2) & 1) ? -p2v : p2v;
+  }
+  if ((R.bits(kLcw3Mask + kLcw3Layers - 1) >> j) & 1) pz = -pz;
+  const double g2 = R.d(0, kLcw3G2);
+  const int wave = t >> 6, lane = t & 63;
+  const double tot = wave_sum(ptot) * g2;
+  const double z = wave_sum(pz) * g2;
+  if (lane == 0) {
+    s_red[wave][0] = tot;
+    s_red[wave][1] = z;
+  }
+  __syncthreads();
+  if (t < 2) {
+    double acc = 0.0;
+    for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
+    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+  }
+}
+
 hipError_t launch_lightcone(const PassArgs& a, dim3 grid, int kind, hipStream_t stream,
                             int* variant) {
   int vdummy = 0;
   if (!variant) variant = &vdummy;
   const int n_tiles = 1 << (a.L_eff - kTileBits);
+  if (a.lc_wide == 2) {
+    // 12-site light-cone pass (C2 form): seven layers, tile bit k = global
+    // bit j-5+k, bits j-6 and j+6 inside the state
+    const int j = a.probe;
+    if (a.meas != kMeasProbe || !a.no_store || a.lc_layers != kLcw3Layers || a.n_obs < 2 ||
+        !a.lc_diag || j < 6 || j + 6 > a.L_real - 1 || a.L_eff > 32 ||
+        (kind != kKindRX && kind != kKindRY))
+      return hipErrorInvalidValue;
+    for (int k = 0; k < kTileBits; ++k)
+      if (a.lc_gb[k] != j - 5 + k) return hipErrorInvalidValue;
+    *variant = kLcVariantWide3;
+    hipLaunchKernelGGL((kind == kKindRX ? dtc_lcw3_final<kKindRX> : dtc_lcw3_final<kKindRY>), grid,
+                       dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+  }
   if (a.lc_wide) {
     // 10-site light-cone pass: six layers, tile bits 0, 1 = global 0, 1, the
     // probe at tile bit 6, twelve distinct global bits inside the state

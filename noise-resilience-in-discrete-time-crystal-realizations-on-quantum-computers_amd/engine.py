@@ -392,10 +392,11 @@ class DtcEngine:
 
     def lightcone_counts(self):
         """Light-cone ends launched since the engine opened, by kernel
-        (dtc_lightcone_counts): 8-site window, 10-site generic, 10-site C2 form."""
-        c = (ctypes.c_int64 * 3)()
+        (dtc_lightcone_counts): 8-site window, 10-site generic, 10-site C2 form,
+        12-site C2 form."""
+        c = (ctypes.c_int64 * 4)()
         _capi.check(self._lib.dtc_lightcone_counts(self._ctx, c))
-        return {"lc8": c[0], "lcw": c[1], "lcw2": c[2]}
+        return {"lc8": c[0], "lcw": c[1], "lcw2": c[2], "lcw3": c[3]}
 
     def device_info(self):
         name = ctypes.create_string_buffer(256)

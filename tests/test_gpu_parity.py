@@ -220,7 +220,8 @@ def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe,
     over an 8-site window (DTC_NO_LCW=1 forces the latter everywhere).  Both
     give the same per-trajectory echo as the oracle (1e-10) and as the engine
     without the merge (DTC_NO_LIGHTCONE=1); pass counts are taken with the
-    dual pass off (DTC_NO_DUAL=1).  The options are read when an
+    dual pass off (DTC_NO_DUAL=1) and the 10-site window's (DTC_NO_LCW3=1:
+    test_lcw3_c2_form covers the 12-site one).  The options are read when an
     engine opens, so each variant runs on its own engine."""
     rng = np.random.default_rng(L * 31 + T)
     hs, phis = random_disorder(rng, L, 2)
@@ -243,7 +244,7 @@ def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe,
     _cmp(got, ref)
     # pass counts without the dual forward+echo-start pass, which also removes
     # passes (the chain's first) and so blurs the light-cone saving
-    single, n_wide = run(["DTC_NO_DUAL"])
+    single, n_wide = run(["DTC_NO_DUAL", "DTC_NO_LCW3"])
     narrow, n_narrow = run(["DTC_NO_LCW", "DTC_NO_DUAL"])
     full, n_full = run(["DTC_NO_LIGHTCONE", "DTC_NO_DUAL"])
     for o in (single, narrow, full):
@@ -271,10 +272,12 @@ def test_lcw2_c2_form(pkg, monkeypatch, L, pol, state, toff, g, p):
     hs, phis = random_disorder(rng, L, 2)
     spec = pkg.SweepSpec(L=L, T=9, hs=hs, phis=phis, g=g, noise_prob=p, use_noise=int(p > 0),
                          polarization=pol, initial_state=state, t_offset=toff)
-    with pkg.DtcEngine(0) as eng:
-        got = eng.autocorr(spec, 3, seed=91)
-        counts = eng.lightcone_counts()
-    assert counts["lcw2"] > 0 and counts["lcw"] == 0, counts
+    with monkeypatch.context() as m:
+        m.setenv("DTC_NO_LCW3", "1")  # the 10-site ends only
+        with pkg.DtcEngine(0) as eng:
+            got = eng.autocorr(spec, 3, seed=91)
+            counts = eng.lightcone_counts()
+    assert counts["lcw2"] > 0 and counts["lcw"] == 0 and counts["lcw3"] == 0, counts
     _cmp(got, c_oracle.autocorr(spec, 3, seed=91))
     with monkeypatch.context() as m:
         m.setenv("DTC_NO_LCW", "1")
@@ -346,3 +349,48 @@ def test_independent_t_matches_oracle(pkg, engine):
     for k in ("fwd", "echo"):
         assert np.abs(got[k] - ref[k]).max() < 1e-10
 
+
+
+@pytest.mark.parametrize("L,T,pol,state,toff,g,p", [
+    (20, 12, "x", "vacuum", 0, 0.97, 0.05),   # BASELINE configs[1]'s kicks and noise
+    (20, 10, "y", "neel", 1, 0.93, 0.1),
+    (21, 11, "x", "neel", 0, 0.91, 0.1),      # 12 + 9 sites
+    (22, 10, "x", "vacuum", 0, 0.95, 0.05),   # three site groups: the form may not fit
+    (20, 9, "y", "vacuum", 1, 0.97, 0.0),     # noiseless: identity frames
+])
+def test_lcw3_c2_form(pkg, monkeypatch, L, T, pol, state, toff, g, p):
+    """The 12-site light-cone end (dtc_lcw3_final: the chain's last six passes
+    as seven layers over j-5 .. j+6, no column bits): where it runs, the echo
+    equals the C oracle per trajectory (1e-10), the 10-site ends
+    (DTC_NO_LCW3) and the 8-site ones (DTC_NO_LCW) to 1e-12, with fewer pass
+    launches than the 10-site form; the forward values are unchanged."""
+    rng = np.random.default_rng(L * 11 + T)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=g, noise_prob=p, use_noise=int(p > 0),
+                         polarization=pol, initial_state=state, t_offset=toff)
+
+    def run(env):
+        with monkeypatch.context() as m:
+            for k in env:
+                m.setenv(k, "1")
+            with pkg.DtcEngine(0) as eng:
+                eng.set_profiling(True)
+                out = eng.autocorr(spec, 3, seed=57)
+                st = eng.kernel_stats()
+                counts = eng.lightcone_counts()
+        n = st[pkg._capi.KERNEL_LO_PASS]["launches"] + st[pkg._capi.KERNEL_HI_PASS]["launches"]
+        return out, counts, n
+
+    got, counts, n3 = run([])
+    _cmp(got, c_oracle.autocorr(spec, 3, seed=57))
+    w10, c10, n10 = run(["DTC_NO_LCW3"])
+    w8, _, _ = run(["DTC_NO_LCW"])
+    for o in (w10, w8):
+        assert np.abs(got["echo"] - o["echo"]).max() < 1e-12
+        assert np.abs(got["fwd"] - o["fwd"]).max() == 0.0
+    assert c10["lcw3"] == 0
+    if L <= 21:  # two site groups: the C2 chains' form
+        assert counts["lcw3"] > 0, counts
+        assert n3 < n10, (n3, n10)
+    else:
+        assert n3 <= n10
