@@ -61,7 +61,8 @@ def main(prof, out, batch, L, bench_args=""):
             ("kdk_dual", ("dtc_kdk_dual",), {"dtc_kdk_dual": 48.0}),
             ("hi_pass", ("dtc_kick_pass",), None),
             ("lightcone_pass", ("dtc_lc_final",), None),
-            ("lightcone_wide_pass", ("dtc_lcw2_final", "dtc_lcw_final"), None)):
+            ("lightcone_wide_pass", ("dtc_lcw2_final", "dtc_lcw_final"), None),
+            ("lightcone_12site_pass", ("dtc_lcw3_final",), None)):
         r = one(names, per_amp)
         if r:
             res[key] = r
