@@ -868,11 +868,12 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
 //   X1  p3 p4 p5 p6 | l0: p3 p4 p5 p6, swap p2 in, p2 | D6 | l1: p3 p4 p5 p2,
 //                     swap m5 in, m5
 //   X2  m4 m3 m2 m1 | l1: m4 m3 m2 m1, swap z0 p1 in, z0 p1 | D5 | l2: z0 p1
-//                     m2 m1, swap m4 m3 back, m4 m3
-//   X3  p2 p3 p4 m3 | l2: p2 p3 p4 | D4 | l3: p2 p3 m3
+//                     m2 m1
+//   X3  p2 p3 p4 m3 | l2: p2 p3 p4 m3, swap m4 in, m4 | D4 | l3: p2 p3 m3
 //   X4  m2 m1 z0 p1 | l3: m2 m1 z0 p1 | D3 | l4: m2 m1 z0 p1, swap p2 in, p2 |
 //                     D2 | l5: m1 z0 p1 | D1 | l6: z0 | probe
-// 41 site kicks, three LDS re-layouts, seven row swaps.  Re-layout slots are
+// 41 site kicks, three LDS re-layouts, six row swaps (a seventh, swapping
+// m4 m3 back in X2, cost 1.7 % of the pass: r4m).  Re-layout slots are
 // the tile index mapped by an invertible GF(2) matrix (lcw3::cv: 4096 slots,
 // the thread's base XOR a compile-time register part): the low five bits of
 // the lane sites' vectors are independent in every layout written (lanes 0..3)
@@ -889,15 +890,16 @@ __host__ __device__ constexpr int cv(int s) {
        : s == p6 ? 512 | 8 : s == p2 ? 1024 | 16 : 2048;
 }
 // layouts: positions 0..3 registers, 4..9 lane bits 0..5, 10..11 wave bits
-enum : int { kX1 = 0, kX1e, kX1f, kX2, kX2s, kX3, kX4, kX4e };
+enum : int { kX1 = 0, kX1e, kX1f, kX2, kX2s, kX3, kX3e, kX4, kX4e };
 __host__ __device__ constexpr int lay_site(int li, int pos) {
-  constexpr int tab[8][12] = {
+  constexpr int tab[9][12] = {
       {p3, p4, p5, p6, m4, m3, m2, m1, p2, m5, z0, p1},   // X1 (load)
       {p3, p4, p5, p2, m4, m3, m2, m1, p6, m5, z0, p1},   // X1e: R3 <-> lane 4
       {m5, p4, p5, p2, m4, m3, m2, m1, p6, p3, z0, p1},   // X1f: R0 <-> lane 5
       {m4, m3, m2, m1, p3, p4, p5, p6, z0, p1, m5, p2},   // X2
       {z0, p1, m2, m1, p3, p4, p5, p6, m4, m3, m5, p2},   // X2s: R0 <-> lane 4, R1 <-> lane 5
-      {p2, p3, p4, m3, m4, p1, m2, m1, z0, m5, p5, p6},   // X3
+      {p2, p3, p4, m3, p1, m2, m1, z0, m4, m5, p5, p6},   // X3
+      {p2, p3, m4, m3, p1, m2, m1, z0, p4, m5, p5, p6},   // X3e: R2 <-> lane 4
       {m2, m1, z0, p1, m4, m3, p5, p6, p2, m5, p3, p4},   // X4
       {p2, m1, z0, p1, m4, m3, p5, p6, m2, m5, p3, p4}};  // X4e: R0 <-> lane 4
   return tab[li][pos];
@@ -1124,20 +1126,19 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
   kick(C1{}, C2{}, LCW3_S(p1));
   kick(C2{}, C2{}, LCW3_S(m2));
   kick(C3{}, C2{}, LCW3_S(m1));
-  swap_reg_lane<0, 16>(v);  // back: register bit 0: m4
-  swap_reg_lane<1, 32>(v);  // register bit 1: m3
-  kick(C0{}, C2{}, LCW3_S(m4));
-  kick(C1{}, C2{}, LCW3_S(m3));
-  xch(LCW3_L(kX2), LCW3_L(kX3));
-  // ---- X3: l2 on p2 p3 p4, D4, l3 on p2 p3 m3 ----
+  xch(LCW3_L(kX2s), LCW3_L(kX3));
+  // ---- X3: l2 on p2 p3 p4 m3, m4 (swapped in), D4, l3 on p2 p3 m3 ----
   kick(C0{}, C2{}, LCW3_S(p2));
   kick(C1{}, C2{}, LCW3_S(p3));
   kick(C2{}, C2{}, LCW3_S(p4));
-  diag2(LCW3_L(kX3), LCW3_L(kT4a), LCW3_L(kT4b));
+  kick(C3{}, C2{}, LCW3_S(m3));
+  swap_reg_lane<2, 16>(v);  // register bit 2: m4 (lane bit 4: p4)
+  kick(C2{}, C2{}, LCW3_S(m4));
+  diag2(LCW3_L(kX3e), LCW3_L(kT4a), LCW3_L(kT4b));
   kick(C0{}, C3{}, LCW3_S(p2));
   kick(C1{}, C3{}, LCW3_S(p3));
   kick(C3{}, C3{}, LCW3_S(m3));
-  xch(LCW3_L(kX3), LCW3_L(kX4));
+  xch(LCW3_L(kX3e), LCW3_L(kX4));
   // ---- X4: l3 on m2 m1 z0 p1, D3, l4, D2, l5, D1, l6 ----
   kick(C0{}, C3{}, LCW3_S(m2));
   kick(C1{}, C3{}, LCW3_S(m1));
