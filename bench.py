@@ -361,7 +361,8 @@ def main(argv=None):
     ap.add_argument("--L", type=int, default=20)
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-traj", type=int, default=0, help="0 = four per host thread (c2)")
+    ap.add_argument("--cpu-traj", type=int, default=0,
+                    help="0 = six per host thread (c2: about 11 s on the GPU box's 16 cores)")
     ap.add_argument("--cpu-tf", type=int, default=20,
                     help="time points of the CPU sample (c2: about 10 s at four trajectories "
                          "per host thread)")
@@ -505,7 +506,7 @@ def main(argv=None):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
         threads = host_cpu_info()["usable_cores"]
-        cpu = cpu_baseline(spec, args.cpu_traj or 4 * threads, args.cpu_tf, threads)
+        cpu = cpu_baseline(spec, args.cpu_traj or 6 * threads, args.cpu_tf, threads)
 
     info = eng.device_info()
     c5 = None
