@@ -59,3 +59,26 @@ def test_l28_coupled_sharded_matches_oracle(pkg, engine, coupled):
     err = np.abs(got["zsite"] - ref["zsite"][0, 0]).max()
     assert err < TOL, err
     assert np.abs(got["norm"] - 1.0).max() < 1e-10
+
+
+def test_l30_coupled_c5_path_matches_oracle(pkg, engine):
+    """The C5 pipeline closer to its L=34 shape: L=30 as 8 virtual shards of
+    2^27 amplitudes (in place, fused kick+exchange) and the whole-state engine,
+    both against one coupled oracle sweep (T=3: the oracle's 2^30-amplitude
+    sweep takes about a minute on the GPU box's 16 cores)."""
+    import torch
+
+    hs, phis = pkg.load_disorder(34, 1, os.path.join(ROOT, "data"))
+    spec = pkg.SweepSpec(L=30, T=3, hs=hs, phis=phis, g=G, polarization="x",
+                         initial_state="neel", use_noise=0)
+    ref = c_oracle.autocorr(spec, 1, want_echo=False, want_zsite=True)
+    got = engine.autocorr(spec, 1, want_echo=False, want_zsite=True)
+    assert np.abs(got["zsite"] - ref["zsite"]).max() < TOL
+    engine.release_buffers()
+    stepper = pkg.sharded.EngineStepper(engine)
+    sh = pkg.sharded.sharded_forward_pipelined(stepper, spec, 3, inplace=True)
+    del stepper
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    assert np.abs(sh["zsite"] - ref["zsite"][0, 0]).max() < TOL
+    assert np.abs(sh["norm"] - 1.0).max() < 1e-10
