@@ -647,8 +647,8 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.n_obs = n_obs;
   A.recs2 = recs2;
   A.dst2 = dst2;
-  if (dst2 && (!recs2 || shape != dtc::kShapeKDK || no_store || basis))
-    return fail(DTC_EINVAL, "internal: a dual pass is a stored K-D-K with its branch's records");
+  if (dst2 && (!recs2 || (shape != dtc::kShapeKDK && shape != dtc::kShapeKD) || no_store || basis))
+    return fail(DTC_EINVAL, "internal: a dual pass is a stored K-D-K / K-D with its branch's records");
   const int kernel = no_store ? DTC_KERNEL_FINAL_PASS
                               : (ps.diag != dtc::kDiagNone ? DTC_KERNEL_LO_PASS : DTC_KERNEL_HI_PASS);
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1651,6 +1651,13 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         std::vector<int> ahead(pl.groups.size());
         for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > ps.d_index;
         Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
+        if (rc.device && ctx->dual) {
+          // device-like noise: the chain starts on the group whose forward
+          // K-D closed the period (the dual pass below)
+          ec.prio.resize(pl.groups.size());
+          for (size_t g = 0; g < pl.groups.size(); ++g)
+            ec.prio[g] = (int)g == ps.group ? -1 : (int)g;
+        }
         const double2* src = F;
         const size_t chain0 = sched.size();
         while (!ec.done()) {
@@ -1690,6 +1697,26 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         // to E: the chain's first read of F and its own pass go away (48 B
         // per amplitude instead of 64).  Not when the chain is one pass (the
         // light-cone end reads F itself).
+        // Device-like noise (no forward layer runs ahead): the forward K-D
+        // on G gives D_p K_p (input), the chain's first pass is D^* K'_1 of
+        // that on G -- K'_1 K_p (input) again, formed by a K-D dual pass.
+        if (ctx->dual && rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
+          Launch& f = sched[chain0 - 1];
+          const Launch& e = sched[chain0];
+          const bool fkd = pass_shape(f.ps) == dtc::kShapeKD && !f.basis && f.src == F &&
+                           (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
+          const bool edk = pass_shape(e.ps) == dtc::kShapeDK && e.ps.lc_w0 < 0 &&
+                           e.ps.group == f.ps.group && e.ps.post.enabled &&
+                           e.ps.post.skip == 0 && f.ps.pre.skip == 0;
+          const int fk = fkd ? pass_kind(rc, f.ps, dtc::kShapeKD) : -1;
+          const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};
+          if (fkd && edk && (fk == dtc::kKindRXU || fk == dtc::kKindRYU) &&
+              fk == pass_kind(rc, e.ps, dtc::kShapeDK) && fk == pass_kind(rc, branch, -1)) {
+            f.ps2 = branch;
+            f.dst2 = E;
+            sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
+          }
+        }
         if (ctx->dual && !rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
           Launch& f = sched[chain0 - 1];
           const Launch& e = sched[chain0];

@@ -457,9 +457,11 @@ template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false, bool SPLIT
           bool DUAL = false>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
-  static_assert(!DUAL || (SHAPE == kShapeKDK && MC <= 1 && !NS &&
-                          (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)),
-                "dual passes: unitary K-D-K, at most the probe");
+  static_assert(!DUAL || (MC <= 1 && !NS &&
+                          ((SHAPE == kShapeKDK &&
+                            (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) ||
+                           (SHAPE == kShapeKD && (KIND == kKindRXU || KIND == kKindRYU)))),
+                "dual passes: unitary K-D-K or device-noise K-D, at most the probe");
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
 #ifdef DTC_PHASE_TIMING
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -859,7 +861,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // device-like noise: a kick layer's deferred Kraus factors (SiteMat),
   // prod over the tile bits k of rho_{k, x_k}, in layout LAY (records rec0 ..)
   constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
-  auto rho_apply = [&](auto lay_tag, int rec0) {
+  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const RecRegs& Rr) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int y = ybase<LAY>(t);
     double rt = 1.0;
@@ -867,15 +869,15 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int k = 0; k < kTileBits; ++k) {
       if (k >= 4 * LAY && k < 4 * LAY + 4) continue;  // register bits
       if (!((NIBS >> (k >> 2)) & 1)) continue;        // no kicks: rho = 1
-      rt *= ((y >> k) & 1) ? R.d(rec0 + k, 4) : R.d(rec0 + k, 3);
+      rt *= ((y >> k) & 1) ? Rr.d(rec0 + k, 4) : Rr.d(rec0 + k, 3);
     }
     double f[kRegs];
     f[0] = rt;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const bool on = (NIBS >> LAY) & 1;
-      const double r0 = on ? R.d(rec0 + 4 * LAY + q, 3) : 1.0;
-      const double r1 = on ? R.d(rec0 + 4 * LAY + q, 4) : 1.0;
+      const double r0 = on ? Rr.d(rec0 + 4 * LAY + q, 3) : 1.0;
+      const double r1 = on ? Rr.d(rec0 + 4 * LAY + q, 4) : 1.0;
 #pragma unroll
       for (int r = 0; r < (1 << q); ++r) {
         f[r | (1 << q)] = f[r] * r1;
@@ -884,8 +886,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      v[r].x *= f[r];
-      v[r].y *= f[r];
+      x[r].x *= f[r];
+      x[r].y *= f[r];
     }
   };
 
@@ -921,6 +923,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     double2 w[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
+    // (device-like noise, a forward K-D: E = K'_1 D^* D K_p (input) -- the
+    // pre-kick's deferred Kraus diagonal first, K'_1's before the store)
+    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::d_lay, RP::O>(w, s_tile, s_half, t);
       apply_nibble<RP::O, KIND>(w, R2, kTileBits);
@@ -934,6 +939,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(w, s_tile, s_half, t);
+    if constexpr (kRho) rho_apply(LIO{}, kTileBits, w, R2);
     // the branch's global factor: i^k w of K_p and of K'_1
     const double2 gE = make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1));
     char* d2 = (char*)(A.dst2 + sbase);
@@ -947,7 +953,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     // reading in the branch's last one
     __syncthreads();
   }
-  if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0);
+  if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, v, R);
   if constexpr (!RP::diag) {
     // no diagonal to carry the kicks' global factor (kick-only pass: no
     // post-kick, so applying it here, before any measurement, is exact)
@@ -986,7 +992,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(v, R, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(v, s_tile, s_half, t);
-    if constexpr (kRho) rho_apply(LIO{}, kTileBits);
+    if constexpr (kRho) rho_apply(LIO{}, kTileBits, v, R);
   } else {
     xch_tile<SPLIT, RP::d_lay, RP::IO>(v, s_tile, s_half, t);
   }
@@ -1107,6 +1113,12 @@ template <int NIBS, int KIND, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kdk_dual(PassArgs A) {
   pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true>(A);
 }
+// its device-noise form: the forward K-D closing a period (device-like noise
+// runs no forward layer ahead) that also starts the echo branch
+template <int NIBS, int KIND, int MC>
+__global__ __launch_bounds__(kThreads, 2) void dtc_kd_dual(PassArgs A) {
+  pass_body<kShapeKD, NIBS, KIND, MC, false, true, true>(A);
+}
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
 DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
@@ -1159,6 +1171,10 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     if constexpr (MC <= 1 && (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) {
       if (shape != kShapeKDK) return hipErrorInvalidValue;
       hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
+      return hipGetLastError();
+    } else if constexpr (MC <= 1 && (KIND == kKindRXU || KIND == kKindRYU)) {
+      if (shape != kShapeKD) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((dtc_kd_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
       return hipGetLastError();
     } else {
       return hipErrorInvalidValue;

@@ -235,3 +235,45 @@ def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
     df = pd.read_csv(full[0])
     for p in ("0", "0.001", "0.01", "0.1"):
         assert df[f"energy_p_{p}"][0] == pytest.approx(float(e0) / 4, abs=1e-12)
+
+
+@pytest.mark.parametrize("L,T,state,pol,toff", [
+    (4, 7, "vacuum", "x", 0),        # one site group: every chain starts on it
+    (14, 6, "neel", "y", 1),
+    (20, 5, "vacuum", "x", 0),       # C3's shape: 12 + 8 sites
+    (21, 4, "neel", "circular_left", 0),  # general kicks: no factored form, no dual pass
+])
+def test_device_dual_pass(pkg, monkeypatch, L, T, state, pol, toff):
+    """Device-like noise runs no forward layer ahead, so a period closes with a
+    forward K-D on group G and the echo chain at that time starts with D^* K'_1
+    on G: dtc_kd_dual forms K'_1 K_p (input) from the K-D's tile after its
+    pre-kick (Kraus diagonals of both layers applied) and stores it to E.  Per
+    trajectory: the oracle's values (1e-10), the unfused schedule's
+    (DTC_NO_DUAL) to 1e-12, and one pass fewer per echo chain when the kicks
+    take the factored form."""
+    rng = np.random.default_rng(L * 3 + T)
+    hs, phis = random_disorder(rng, L, 2)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, polarization=pol,
+                         initial_state=state, t_offset=toff, device=harsh_device(pkg, L))
+
+    def run(no_dual):
+        with monkeypatch.context() as m:
+            if no_dual:
+                m.setenv("DTC_NO_DUAL", "1")
+            with pkg.DtcEngine(0) as eng:
+                eng.set_profiling(True)
+                out = eng.autocorr(spec, 3, seed=29)
+                st = eng.kernel_stats()
+        return out, st[pkg._capi.KERNEL_LO_PASS]["launches"] + st[pkg._capi.KERNEL_HI_PASS]["launches"]
+
+    got, n_dual = run(False)
+    ref, n_single = run(True)
+    want = c_oracle.autocorr(spec, 3, seed=29)
+    for k in want:
+        assert float(np.abs(got[k] - want[k]).max()) < 1e-10, k
+    assert np.abs(got["echo"] - ref["echo"]).max() < 1e-12
+    assert np.abs(got["fwd"] - ref["fwd"]).max() < 1e-13
+    if pol == "circular_left":
+        assert n_dual == n_single
+    else:
+        assert n_dual < n_single
