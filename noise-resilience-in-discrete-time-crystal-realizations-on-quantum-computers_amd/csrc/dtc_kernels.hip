@@ -1111,7 +1111,11 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
 // opaque per-thread bases keep the addresses out of the register budget)
 template <int NIBS, int KIND, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kdk_dual(PassArgs A) {
+#ifdef DTC_DUAL_FULL
+  pass_body<kShapeKDK, NIBS, KIND, MC, false, !((DTC_DUAL_FULL >> NIBS) & 1), true>(A);
+#else
   pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true>(A);
+#endif
 }
 // its device-noise form: the forward K-D closing a period (device-like noise
 // runs no forward layer ahead) that also starts the echo branch
