@@ -1108,14 +1108,11 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
 }
 // a forward K-D-K that also starts an echo branch (pass_body DUAL): two
 // tiles in registers, so two workgroups per CU; half-tile re-layouts (their
-// opaque per-thread bases keep the addresses out of the register budget)
+// opaque per-thread bases keep the addresses out of the register budget: with
+// full-tile ones the <7> form takes 256 VGPRs and spills 27, r4u: 9.9 -> 11.5 ms)
 template <int NIBS, int KIND, int MC>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kdk_dual(PassArgs A) {
-#ifdef DTC_DUAL_FULL
-  pass_body<kShapeKDK, NIBS, KIND, MC, false, !((DTC_DUAL_FULL >> NIBS) & 1), true>(A);
-#else
   pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true>(A);
-#endif
 }
 // its device-noise form: the forward K-D closing a period (device-like noise
 // runs no forward layer ahead) that also starts the echo branch
