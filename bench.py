@@ -582,8 +582,9 @@ def main(argv=None):
             "kick_pass": {"launches": hi["launches"], "avg_ms": avg_hi * 1e3,
                           "bytes_per_launch": hi_bytes,
                           "GBps": hi_bytes / avg_hi / 1e9 if hi["launches"] else None,
-                          "note": "first pass of a sweep: basis states formed in registers, "
-                                  "store only (16 B/amp)"},
+                          "note": "kick-only passes: the sweep's first (basis states formed "
+                                  "in registers, store only, 16 B/amp) and, under device-like "
+                                  "noise, the forward chain's kick passes (32 B/amp)"},
             "final_pass": {"launches": stats[4]["launches"], "avg_ms":
                            stats[4]["total_ms"] / max(1, stats[4]["launches"]),
                            "GBps": stats[4]["bytes"] / (stats[4]["total_ms"] / 1e3) / 1e9
