@@ -277,3 +277,28 @@ def test_device_dual_pass(pkg, monkeypatch, L, T, state, pol, toff):
         assert n_dual == n_single
     else:
         assert n_dual < n_single
+
+
+def test_device_dual_batches_and_t_first(pkg, engine):
+    """The device dual pass under the schedule's other shapes: two instances,
+    batches that split the octets (batch invariance is exact), echo-only and
+    t_first > 0 runs (the chains at t < t_first are not built, so the fold
+    lands on other forward passes), each against the oracle per trajectory."""
+    rng = np.random.default_rng(41)
+    hs, phis = random_disorder(rng, 16, 2)
+    spec = pkg.SweepSpec(L=16, T=6, hs=hs, phis=phis, g=0.91, polarization="x",
+                         initial_state="neel", device=harsh_device(pkg, 16))
+    a = engine.autocorr(spec, 10, seed=13, batch=20)
+    b = engine.autocorr(spec, 10, seed=13, batch=3)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    ref = c_oracle.autocorr(spec, 10, seed=13)
+    for k in ref:
+        assert float(np.abs(a[k] - ref[k]).max()) < 1e-10, k
+    e = engine.autocorr(spec, 10, seed=13, want_fwd=False)
+    assert np.abs(e["echo"] - ref["echo"]).max() < 1e-10
+    late = engine.autocorr(spec, 10, seed=13, t_first=3)
+    ref_late = c_oracle.autocorr(spec, 10, seed=13, t_first=3)
+    for k in ref_late:
+        assert float(np.abs(late[k] - ref_late[k]).max()) < 1e-10, k
+        assert np.abs(late[k][..., 3:] - a[k][..., 3:]).max() < 1e-12, k
