@@ -1700,36 +1700,27 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         // Device-like noise (no forward layer runs ahead): the forward K-D
         // on G gives D_p K_p (input), the chain's first pass is D^* K'_1 of
         // that on G -- K'_1 K_p (input) again, formed by a K-D dual pass.
-        if (ctx->dual && rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
+        if (ctx->dual && sched.size() - chain0 >= 2 && chain0 >= 1) {
           Launch& f = sched[chain0 - 1];
           const Launch& e = sched[chain0];
-          const bool fkd = pass_shape(f.ps) == dtc::kShapeKD && !f.basis && f.src == F &&
+          const int fs = rc.device ? dtc::kShapeKD : dtc::kShapeKDK;
+          const int es = rc.device ? dtc::kShapeDK : dtc::kShapeKDK;
+          // (the dual kernels carry the probe at most: not with per-site Z)
+          const bool fok = pass_shape(f.ps) == fs && !f.basis && f.src == F &&
                            (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
-          const bool edk = pass_shape(e.ps) == dtc::kShapeDK && e.ps.lc_w0 < 0 &&
-                           e.ps.group == f.ps.group && e.ps.post.enabled &&
-                           e.ps.post.skip == 0 && f.ps.pre.skip == 0;
-          const int fk = fkd ? pass_kind(rc, f.ps, dtc::kShapeKD) : -1;
+          const bool eok =
+              pass_shape(e.ps) == es && e.ps.lc_w0 < 0 && e.ps.group == f.ps.group &&
+              e.ps.post.enabled &&
+              (rc.device ? e.ps.post.skip == 0 && f.ps.pre.skip == 0
+                         : e.ps.pre.mode == dtc::kKickUndo && e.ps.pre.skip == 0 &&
+                               f.ps.post.skip == 0);
+          const int fk = fok ? pass_kind(rc, f.ps, fs) : -1;
+          const bool kind_ok = rc.device ? (fk == dtc::kKindRXU || fk == dtc::kKindRYU)
+                                         : (fk == dtc::kKindRX || fk == dtc::kKindRY ||
+                                            fk == dtc::kKindGen);
           const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};
-          if (fkd && edk && (fk == dtc::kKindRXU || fk == dtc::kKindRYU) &&
-              fk == pass_kind(rc, e.ps, dtc::kShapeDK) && fk == pass_kind(rc, branch, -1)) {
-            f.ps2 = branch;
-            f.dst2 = E;
-            sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
-          }
-        }
-        if (ctx->dual && !rc.device && sched.size() - chain0 >= 2 && chain0 >= 1) {
-          Launch& f = sched[chain0 - 1];
-          const Launch& e = sched[chain0];
-          // (the dual kernel carries the probe at most: not with per-site Z)
-          const bool fkdk = pass_shape(f.ps) == dtc::kShapeKDK && !f.basis && f.src == F &&
-                            (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
-          const bool ekdk = pass_shape(e.ps) == dtc::kShapeKDK && e.ps.lc_w0 < 0 &&
-                            e.ps.group == f.ps.group && e.ps.pre.mode == dtc::kKickUndo &&
-                            e.ps.post.enabled && e.ps.pre.skip == 0 && f.ps.post.skip == 0;
-          const int fk = fkdk ? pass_kind(rc, f.ps, dtc::kShapeKDK) : -1;
-          const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};
-          if (fkdk && ekdk && (fk == dtc::kKindRX || fk == dtc::kKindRY || fk == dtc::kKindGen) &&
-              fk == pass_kind(rc, e.ps, dtc::kShapeKDK) && fk == pass_kind(rc, branch, -1)) {
+          if (fok && eok && kind_ok && fk == pass_kind(rc, e.ps, es) &&
+              fk == pass_kind(rc, branch, -1)) {
             f.ps2 = branch;
             f.dst2 = E;
             sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
