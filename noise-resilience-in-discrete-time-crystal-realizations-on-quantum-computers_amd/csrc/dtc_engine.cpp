@@ -1715,7 +1715,8 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                          : e.ps.pre.mode == dtc::kKickUndo && e.ps.pre.skip == 0 &&
                                f.ps.post.skip == 0);
           const int fk = fok ? pass_kind(rc, f.ps, fs) : -1;
-          const bool kind_ok = rc.device ? (fk == dtc::kKindRXU || fk == dtc::kKindRYU)
+          const bool kind_ok = rc.device ? (fk == dtc::kKindRXU || fk == dtc::kKindRYU ||
+                                            fk == dtc::kKindGen)
                                          : (fk == dtc::kKindRX || fk == dtc::kKindRY ||
                                             fk == dtc::kKindGen);
           const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};

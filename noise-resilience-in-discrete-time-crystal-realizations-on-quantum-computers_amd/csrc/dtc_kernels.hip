@@ -460,7 +460,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   static_assert(!DUAL || (MC <= 1 && !NS &&
                           ((SHAPE == kShapeKDK &&
                             (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) ||
-                           (SHAPE == kShapeKD && (KIND == kKindRXU || KIND == kKindRYU)))),
+                           (SHAPE == kShapeKD &&
+                            (KIND == kKindRXU || KIND == kKindRYU || KIND == kKindGen)))),
                 "dual passes: unitary K-D-K or device-noise K-D, at most the probe");
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
 #ifdef DTC_PHASE_TIMING
@@ -1169,17 +1170,20 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     }
   }
   if (a.dst2) {
+    // K-D-K: unitary kicks; K-D: device-like noise (factored or general kicks)
     if constexpr (MC <= 1 && (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) {
-      if (shape != kShapeKDK) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
-      return hipGetLastError();
-    } else if constexpr (MC <= 1 && (KIND == kKindRXU || KIND == kKindRYU)) {
-      if (shape != kShapeKD) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((dtc_kd_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
-      return hipGetLastError();
-    } else {
-      return hipErrorInvalidValue;
+      if (shape == kShapeKDK) {
+        hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
+        return hipGetLastError();
+      }
     }
+    if constexpr (MC <= 1 && (KIND == kKindRXU || KIND == kKindRYU || KIND == kKindGen)) {
+      if (shape == kShapeKD) {
+        hipLaunchKernelGGL((dtc_kd_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
+        return hipGetLastError();
+      }
+    }
+    return hipErrorInvalidValue;
   }
   switch (shape) {
     case kShapeKDK:
