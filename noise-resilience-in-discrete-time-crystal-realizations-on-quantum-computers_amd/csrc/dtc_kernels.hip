@@ -1135,7 +1135,14 @@ DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
 DTC_DEFINE_FINAL(dtc_kdk_final, kShapeKDK)
 DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
 DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
-DTC_DEFINE_FINAL(dtc_kick_final, kShapeK)
+// the kick-only end (device-like noise chains end in one) at three workgroups
+// per CU with the half-tile re-layouts: a read-only pass has no stores to
+// overlap its loads with, so the third workgroup's loads do (r4zc: C3's
+// <7> 3.80 -> 3.03 ms, <6> 3.24 -> 2.85 ms)
+template <int NIBS, int KIND>
+__global__ __launch_bounds__(kThreads, 3) void dtc_kick_final(PassArgs A) {
+  pass_body<kShapeK, NIBS, KIND, 1, true, true>(A);
+}
 #undef DTC_DEFINE_FINAL
 // The energy sweep's last pass (one kick layer past the last period, for the
 // X of its group at the last time point): measures, stores nothing.
