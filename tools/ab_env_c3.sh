@@ -1,0 +1,21 @@
+#!/bin/bash
+# Development A/B of engine environment switches (not the product): bench.py C2
+# under rocprofv3 --kernel-trace --stats once per setting.
+# Usage (GPU box, repo root): bash tools/ab_env.sh <tag> "VAR=0" "VAR=1" ...
+set -o pipefail
+TAG=$1; shift
+R=$(pwd); O=$R/gpurun_out; mkdir -p $O; export TMPDIR=/tmp
+cd /tmp
+i=0
+for setting in "$@"; do
+  i=$((i+1)); n=${TAG}_$i
+  ( export $setting; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_$n -o kt -- python $R/bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/ab_$n.json 2> $O/ab_$n.err ) || { echo "$setting failed"; exit 1; }
+  python - "$O/ab_$n" "$setting" <<'PY'
+import json, sys, pandas as pd
+d = json.load(open(sys.argv[1] + ".json"))
+k = pd.read_csv(sys.argv[1] + "/kt_kernel_stats.csv")
+k = k[k.Name.str.contains("kdk")]
+print(sys.argv[2], round(d["value"]), round(d["roofline"]["achieved"]),
+      " ".join(f"{r.Name.split('<')[1].split('>')[0].replace(' ', '')}={r.AverageNs / 1e6:.4f}" for r in k.itertuples()))
+PY
+done
