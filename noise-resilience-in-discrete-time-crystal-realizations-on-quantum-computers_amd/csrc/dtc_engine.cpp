@@ -1714,7 +1714,18 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
               (rc.device ? e.ps.post.skip == 0 && f.ps.pre.skip == 0
                          : e.ps.pre.mode == dtc::kKickUndo && e.ps.pre.skip == 0 &&
                                f.ps.post.skip == 0);
-          const int fk = fok ? pass_kind(rc, f.ps, fs) : -1;
+          // the fold is exact only when the chain's first pass conjugates the
+          // forward's diagonal (one table per instance; d_index only counts
+          // each chain's own periods) and, in the unitary case, undoes exactly
+          // the forward's post-kick: check it, so a different chain order
+          // falls back to the separate passes instead of folding wrongly
+          const bool same_d = f.ps.diag == dtc::kDiagFwd && e.ps.diag == dtc::kDiagConj;
+          const bool undoes_post =
+              rc.device || (f.ps.post.enabled && f.ps.post.mode == dtc::kKickForward &&
+                            e.ps.pre.row == f.ps.post.row &&
+                            e.ps.pre.stream == f.ps.post.stream &&
+                            e.ps.pre.rng_period == f.ps.post.rng_period);
+          const int fk = (fok && same_d && undoes_post) ? pass_kind(rc, f.ps, fs) : -1;
           const bool kind_ok = rc.device ? (fk == dtc::kKindRXU || fk == dtc::kKindRYU ||
                                             fk == dtc::kKindGen)
                                          : (fk == dtc::kKindRX || fk == dtc::kKindRY ||
@@ -2504,14 +2515,20 @@ int dtc_shard_kick_exchange_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc
   if (pre_mask & ~low) return fail(DTC_EINVAL, "slice kick mask reaches the chunk/slice bits");
   RunCfg rc = shard_runcfg(pr, nz, sh, seed, traj);
   const Plan& pl = rc.pl;
-  // the group whose pass goes last carries the exchange (a unitary kick kind)
+  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
+  if (period < 1 || period > n_rows) return fail(DTC_EINVAL, "period outside kick table");
+  // the group whose pass goes last carries the exchange (a unitary kick kind,
+  // classified on the row that pass actually launches; launch_kick_swap takes
+  // 1 <= k <= 6 chunk bits, other shapes run the two calls)
   int last = -1;
   for (size_t g = 0; g < pl.groups.size(); ++g)
     if (pre_mask & group_bits(pl.groups[g])) last = (int)g;
-  bool fuse = last >= 0;
+  bool fuse = last >= 0 && k >= 1 && k <= 6;
   if (fuse) {
+    const Group& G = pl.groups[last];
     PassSpec ps{last, no_kick(), no_kick(), dtc::kDiagNone, 0};
-    ps.pre = dtc::KickDesc{1, 0, dtc::kKickForward, dtc::kStreamForward, 1u, 0u};
+    ps.pre = dtc::KickDesc{1, period - 1, dtc::kKickForward, dtc::kStreamForward,
+                           (uint32_t)period, skip_bits(G, pre_mask)};
     const int kind = pass_kind(rc, ps, dtc::kShapeK);
     fuse = kind == dtc::kKindRX || kind == dtc::kKindRY || kind == dtc::kKindGen;
   }
@@ -2520,8 +2537,6 @@ int dtc_shard_kick_exchange_slice(dtc_ctx* ctx, const dtc_problem* pr, const dtc
                                  slice, state));
     return dtc_shard_exchange_slice(ctx, sh, slice_bits, slice, state);
   }
-  const int n_rows = std::max(1, pr->T - 1 + pr->t_offset);
-  if (period < 1 || period > n_rows) return fail(DTC_EINVAL, "period outside kick table");
   DTC_HIP(hipSetDevice(ctx->device));
   DTC_TRY(shard_kick_tables(ctx, pr, sh, rc));
   rc.L_eff_override = nsub;

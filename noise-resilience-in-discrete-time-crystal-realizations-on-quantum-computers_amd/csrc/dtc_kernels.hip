@@ -1448,7 +1448,10 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_kick_swap_pass(PassArgs A, in
   };
   kick(v);
   store(v, p2);  // (r, c) -> (c, r); the diagonal piece in place
-  if (b2 != b1) {
+  if (b2 != b1) {  // uniform across the workgroup
+    // w's first re-layout writes slots other threads may still be reading in
+    // v's last one (as in dtc_kdk_dual)
+    __syncthreads();
     kick(w);
     store(w, p1);
   }

@@ -410,6 +410,7 @@ class _SliceExchange:
 
         self.W, self.S, self.rank, self.world, self.group = W, S, rank, world, group
         self.inplace, self.slice_bits = inplace, slice_bits
+        self.fused = False  # set by kick_and_swap (fused in-place kick+exchange)
         self.stepper = stepper
         self.cuda = hasattr(stepper, "stream")
         self.eng = stepper.stream() if self.cuda else None
@@ -479,7 +480,10 @@ class _SliceExchange:
 
     def kick_and_swap(self, s, fn):
         """In place: ``fn`` kicks slice s and exchanges it in one step (the
-        fused kick+exchange pass, ordered on the engine stream)."""
+        fused kick+exchange pass, ordered on the engine stream).  Its window
+        then holds the slice's kicks too: ``stats`` reports it under
+        ``kick_exchange_ms``, not ``exchange_ms``."""
+        self.fused = True
         if self.cuda:
             self._mark_start(s, self.eng)
         fn()
@@ -535,8 +539,10 @@ def sharded_forward_pipelined(stepper, spec: SweepSpec, n_global: int, *, inst: 
     or ``(A, None)``.
 
     ``stats`` (dict, optional) receives the per-period exchange windows (ms,
-    side-stream events; engine-stream events in place) and the per-period wall
-    of the engine stream (``period_ms``) on the GPU."""
+    side-stream events; engine-stream events in place) as ``exchange_ms`` and
+    the per-period wall of the engine stream (``period_ms``) on the GPU; with
+    the fused in-place kick+exchange the windows include the slice kicks and go
+    to ``kick_exchange_ms`` instead (``exchange_ms`` is then empty)."""
     return _run_rank(_pipelined_rank(stepper, spec, n_global, inst=inst, traj=traj, seed=seed,
                                      rank=rank, world=world, group=group, buffers=buffers,
                                      stats=stats, inplace=inplace,
@@ -692,7 +698,10 @@ def _pipelined_rank(stepper, spec: SweepSpec, n_global: int, *, inst: int = 0, t
         if t >= 0:
             norm[t], zs[t] = z[p, 0], z[p, 1:]
     if stats is not None:
-        stats["exchange_ms"] = xch.exchange_ms() if xch.cuda else []
+        windows = xch.exchange_ms() if xch.cuda else []
+        # fused in place: the windows span the slice kicks as well as the swaps
+        stats["exchange_ms"] = [] if xch.fused else windows
+        stats["kick_exchange_ms"] = windows if xch.fused else []
         stats["period_ms"] = ([a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:])]
                               if marks else [])
     fac = (1.0 - spec.p) ** N_ANCILLA_NOISY_GATES
