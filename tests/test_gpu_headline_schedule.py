@@ -44,8 +44,19 @@ def _spec(pkg):
                          initial_state="vacuum")
 
 
+def _free_device_memory(engine):
+    """Earlier GPU tests leave large buffers behind (the shared engine's batch
+    buffers, torch's cached blocks of the L=34 state): B=1024 L=20 states need
+    32 GiB for F and E."""
+    import torch
+
+    engine.release_buffers()
+    torch.cuda.empty_cache()
+
+
 @pytest.fixture(scope="module")
-def headline(pkg):
+def headline(pkg, engine):
+    _free_device_memory(engine)
     spec = _spec(pkg)
     oracle = {}
     for lo, hi in RANGES:
@@ -66,7 +77,7 @@ def _check(got, oracle, off, keys=("fwd", "echo"), t_first=0):
             assert err < TOL, (k, g, err)
 
 
-def test_headline_schedule_matches_oracle(pkg, headline):
+def test_headline_schedule_matches_oracle(pkg, engine, headline):
     """Both batches of the bench's first two steps, as bench.py runs them: the
     sampled ids equal the oracle at 1e-10 (fwd and echo, t = 0..29); the
     12-site light-cone end and the dual pass both ran."""
@@ -80,6 +91,7 @@ def test_headline_schedule_matches_oracle(pkg, headline):
                 first = got
         counts = eng.lightcone_counts()
         lo = eng.kernel_stats()[pkg._capi.KERNEL_LO_PASS]
+        eng.release_buffers()
     assert counts["lcw3"] > 0, counts
     # every echo chain of t >= 7 ends in the 12-site form (t = 7 .. 29 per batch)
     assert counts["lcw3"] >= 2 * 23, counts
@@ -90,6 +102,7 @@ def test_headline_schedule_matches_oracle(pkg, headline):
             eng.set_profiling(True)
             ref = eng.autocorr(spec, B, seed=SEED, traj_offset=0, batch=B)
             lo_ref = eng.kernel_stats()[pkg._capi.KERNEL_LO_PASS]
+            eng.release_buffers()
     finally:
         del os.environ["DTC_NO_DUAL"]
     n_dual = lo_ref["launches"] - lo["launches"] // 2
@@ -111,3 +124,4 @@ def test_headline_schedule_echo_only_and_t_first(pkg, engine, headline):
     late = engine.autocorr(spec, B, seed=SEED, traj_offset=0, batch=B, t_first=20)
     _check(late, oracle, 0, t_first=20)
     assert not np.any(late["echo"][..., :20])
+    engine.release_buffers()
