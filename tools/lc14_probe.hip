@@ -46,20 +46,16 @@ __device__ __forceinline__ int ybase_n(int t) {
 // XOR swizzle: lane bits spread over the banks in every layout
 __host__ __device__ constexpr int swz(int y) { return y ^ ((y >> 5) & 31) ^ ((y >> 10) & 15); }
 
-template <int TB, int WPC>
-__global__ __launch_bounds__(1 << (TB - 4), WPC) void k_lc(const double2* __restrict__ st, int L,
-                                                          int w0, int og, int batch,
-                                                          const double* __restrict__ coefs,
-                                                          const double2* __restrict__ tabs,
-                                                          double* __restrict__ out) {
+template <int TB>
+__device__ __forceinline__ void lc_body(const double2* __restrict__ st, int L, int w0, int og,
+                                        int batch, const double* __restrict__ coefs,
+                                        const double2* __restrict__ tabs, double* __restrict__ out,
+                                        double* s_x, double2* s_tab, unsigned bx, unsigned by) {
   constexpr int NT = 1 << (TB - 4);
-  constexpr int NTILE = 1 << TB;
-  __shared__ double s_x[NTILE];
-  __shared__ double2 s_tab[512];
   const int t = threadIdx.x;
   const int tile_bits = L - TB;
-  const int64_t b = ((int64_t)blockIdx.y << 3) | (blockIdx.x & 7);
-  const int64_t tile = blockIdx.x >> 3;
+  const int64_t b = ((int64_t)by << 3) | (bx & 7);
+  const int64_t tile = bx >> 3;
   if (b >= batch) return;
   // tile id: global bits 0 .. w0-1 and w0+TB .. L-1
   const int64_t tbase = (tile & ((1 << w0) - 1)) | ((tile >> w0) << (w0 + TB));
@@ -184,8 +180,104 @@ __global__ __launch_bounds__(1 << (TB - 4), WPC) void k_lc(const double2* __rest
   tot = wave_sum(tot);
   z = wave_sum(z);
   if ((t & 63) == 0) {
-    out[(blockIdx.y * gridDim.x + blockIdx.x) * 2 % (1 << 22)] = tot + z;
+    out[(by * 4096 + bx) * 2 % (1 << 22)] = tot + z;
   }
+}
+
+template <int TB, int WPC>
+__global__ __launch_bounds__(1 << (TB - 4), WPC) void k_lc(const double2* __restrict__ st, int L,
+                                                          int w0, int og, int batch,
+                                                          const double* __restrict__ coefs,
+                                                          const double2* __restrict__ tabs,
+                                                          double* __restrict__ out) {
+  __shared__ double s_x[1 << TB];
+  __shared__ double2 s_tab[512];
+  lc_body<TB>(st, L, w0, og, batch, coefs, tabs, out, s_x, s_tab, blockIdx.x, blockIdx.y);
+}
+
+// A synthetic 12-site K-D-K (the product's dtc_kdk_pass3<7> shape): 16
+// nontemporal 16-B loads of a contiguous 4096-amplitude tile in layout 1
+// (lanes = tile bits 0..3, 8..11), 24 kicks in six 4-site rounds with four
+// half-tile re-layouts, one diagonal lookup per amplitude, 16 nontemporal
+// stores in place.
+__device__ __forceinline__ void kdk_body(double2* __restrict__ st, int L, int og, int batch,
+                                         const double* __restrict__ coefs,
+                                         const double2* __restrict__ tabs, double* s_x,
+                                         double2* s_tab, unsigned bx, unsigned by) {
+  const int t = threadIdx.x;
+  const int64_t b = ((int64_t)by << 3) | (bx & 7);
+  const int64_t tile = bx >> 3;
+  if (b >= batch) return;
+  RecRegs R;
+  {
+    const int lane = t & 63;
+    R.rv[0] = coefs[(b * 64 + lane) * 4 % 4096];
+    R.rv[1] = coefs[(b * 64 + lane) * 4 % 4096 + 1];
+    R.rv[2] = coefs[(b * 64 + lane) * 4 % 4096 + 2];
+    R.rv[3] = coefs[(b * 64 + lane) * 4 % 4096 + 3];
+  }
+  const double2 tv = tabs[t & 255];
+  char* base = (char*)(st + state_base(b, (int64_t)1 << L, og));
+  const int64_t tb = tile << 12;
+  auto addr = [&](int r) { return base + (octet_spread(tb | tile_y<1>(t, r), og) << 4); };
+  double2 v[kRegs];
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    const d2v w = __builtin_nontemporal_load((const d2v*)addr(r));
+    v[r] = make_double2(w.x, w.y);
+  }
+  s_tab[t] = tv;
+  auto nib = [&](auto q0) {
+    constexpr int K = decltype(q0)::value;
+    layer_f<kKindRX, 0, 0>(v, R.d(0, K + 0));
+    layer_f<kKindRX, 0, 1>(v, R.d(0, K + 1));
+    layer_f<kKindRX, 0, 2>(v, R.d(0, K + 2));
+    layer_f<kKindRX, 0, 3>(v, R.d(0, K + 3));
+  };
+  nib(std::integral_constant<int, 0>{});
+  exchange_split<1, 0>(v, s_x, t);
+  nib(std::integral_constant<int, 4>{});
+  exchange_split<0, 2>(v, s_x, t);
+  nib(std::integral_constant<int, 8>{});
+  {
+    int ba = t & 255;
+    asm volatile("" : "+v"(ba));
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], s_tab[(ba ^ (r * 7)) & 255]);
+  }
+  nib(std::integral_constant<int, 12>{});
+  exchange_split<2, 0>(v, s_x, t);
+  nib(std::integral_constant<int, 16>{});
+  exchange_split<0, 1>(v, s_x, t);
+  nib(std::integral_constant<int, 20>{});
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    d2v w = {v[r].x, v[r].y};
+    __builtin_nontemporal_store(w, (d2v*)addr(r));
+  }
+}
+
+__global__ __launch_bounds__(256, 3) void k_kdk(double2* __restrict__ st, int L, int og, int batch,
+                                                 const double* __restrict__ coefs,
+                                                 const double2* __restrict__ tabs) {
+  __shared__ double s_x[4096];
+  __shared__ double2 s_tab[512];
+  kdk_body(st, L, og, batch, coefs, tabs, s_x, s_tab, blockIdx.x, blockIdx.y);
+}
+
+// Both in one launch: groups of eight blocks (one octet tile, one block per
+// XCD) alternate between a K-D-K tile of `kst` and a light-cone tile of `lst`,
+// so every CU holds a mix of memory-bound and VALU-bound workgroups.
+__global__ __launch_bounds__(256, 3) void k_fused(double2* __restrict__ kst,
+                                                   const double2* __restrict__ lst, int L, int og,
+                                                   int batch, const double* __restrict__ coefs,
+                                                   const double2* __restrict__ tabs,
+                                                   double* __restrict__ out) {
+  __shared__ double s_x[4096];
+  __shared__ double2 s_tab[512];
+  const unsigned g = blockIdx.x >> 3, bx = ((g >> 1) << 3) | (blockIdx.x & 7);
+  if (g & 1) lc_body<12>(lst, L, 5, og, batch, coefs, tabs, out, s_x, s_tab, bx, blockIdx.y);
+  else kdk_body(kst, L, og, batch, coefs, tabs, s_x, s_tab, bx, blockIdx.y);
 }
 
 int main(int argc, char** argv) {
@@ -194,8 +286,11 @@ int main(int argc, char** argv) {
   double2* st;
   double *coefs, *out;
   double2* tabs;
+  double2* st2;
   CHECK(hipMalloc(&st, n * 16));
   CHECK(hipMemset(st, 0, n * 16));
+  CHECK(hipMalloc(&st2, n * 16));
+  CHECK(hipMemset(st2, 0, n * 16));
   CHECK(hipMalloc(&coefs, 4096 * 8));
   CHECK(hipMemset(coefs, 0, 4096 * 8));
   CHECK(hipMalloc(&tabs, 512 * 16));
@@ -230,6 +325,23 @@ int main(int argc, char** argv) {
   if (run("14-bit program, 1 WG/CU (w0 = 3)", [&] {
         hipLaunchKernelGGL((k_lc<14, 1>), dim3(8u << (L - 14), oct), dim3(1024), 0, 0, st, L, 3, og,
                            B, coefs, tabs, out);
+      }))
+    return 1;
+  if (run("synthetic 12-site K-D-K, 3 WG/CU", [&] {
+        hipLaunchKernelGGL(k_kdk, dim3(8u << (L - 12), oct), dim3(256), 0, 0, st2, L, og, B, coefs,
+                           tabs);
+      }))
+    return 1;
+  if (run("K-D-K then lcw3 program (two launches)", [&] {
+        hipLaunchKernelGGL(k_kdk, dim3(8u << (L - 12), oct), dim3(256), 0, 0, st2, L, og, B, coefs,
+                           tabs);
+        hipLaunchKernelGGL((k_lc<12, 4>), dim3(8u << (L - 12), oct), dim3(256), 0, 0, st, L, 5, og,
+                           B, coefs, tabs, out);
+      }))
+    return 1;
+  if (run("K-D-K + lcw3 program fused (one launch, 3 WG/CU)", [&] {
+        hipLaunchKernelGGL(k_fused, dim3(16u << (L - 12), oct), dim3(256), 0, 0, st2, st, L, og, B,
+                           coefs, tabs, out);
       }))
     return 1;
   if (run("12-bit lcw3 program, 4 WG/CU (again)", [&] {
