@@ -833,6 +833,10 @@ def main_c5(args):
             dist.destroy_process_group()
         return
     achieved = pass_bytes / (pass_ms / 1e3) / 1e9 if pass_ms else 0.0
+    # PMC summary of this line (tools/pmc_traffic.sh with BENCH_ARGS="--config
+    # c5", one GPU: tools/pmc_summary.py's per-period form), scaled to this run
+    c5_traffic, c5_traffic_src = (read_traffic(pass_bytes, "_pmc_c5.json")
+                                  if inplace else (None, None))
     # a per-period model for judging the 8-GPU run: the passes at
     # this rank's measured pass rate, plus the exchange of (W-1)/W of the shard
     # over 7 xGMI links at 7 x 153 GB/s (MI355X_MICROARCH/the task's figure)
@@ -853,7 +857,9 @@ def main_c5(args):
         "roofline": {"bound": "hbm",
                      "kernel": "pass kernels (slice kicks + fused K-D-K), per-rank shard",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": c5_traffic, "traffic_source": c5_traffic_src,
+                     "traffic_unit": "HBM bytes per period (PMC, this rank's shard)",
                      "algorithmic_bytes_per_period": pass_bytes},
         "period_ms": elapsed / n_per * 1e3,
         "pass_ms_per_period": pass_ms,

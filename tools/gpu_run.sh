@@ -9,6 +9,9 @@
 #   smoke              __graft_entry__.smoke()
 #   tests[:<expr>]     pytest -m gpu [-k <expr>] -> <tag>_gputest.txt
 #   ab:<VAR=v>,<VAR=v> interleaved env A/B of the C2 line under rocprof (tools/ab_env.sh)
+#   stage              copy this call's PMC summaries (gpurun_out/<tag>*_pmc*.json) into
+#                      profiles/ of the box's copy, so later bench steps cite them
+#   exec:<file>        run gpu_bin/<file> (a probe built in the container) -> <tag>_<file>.txt
 set -o pipefail
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -41,6 +44,13 @@ for step in "$@"; do
     ab:*)
       IFS=, read -ra settings <<< "${step#ab:}"
       bash tools/ab_env.sh $TAG "${settings[@]}" || exit 1 ;;
+    stage)
+      cp $O/${TAG}*_pmc*.json profiles/ || exit 1
+      ls profiles/${TAG}*_pmc*.json ;;
+    exec:*)
+      f=${step#exec:}
+      timeout -k 10 300 gpu_bin/$f > $O/${TAG}_$f.txt 2>&1 || { tail -5 $O/${TAG}_$f.txt; exit 1; }
+      cat $O/${TAG}_$f.txt ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -52,6 +52,33 @@ def main(prof, out, batch, L, bench_args=""):
                 "algorithmic_bytes_per_launch": alg_tot / n,
                 "ratio_to_algorithmic": hbm / (alg_tot / n)}
 
+    if "--config c5" in bench_args:
+        # one L=34 state over virtual shards: every pass kernel of the run (slice
+        # kicks, the fused kick+exchange, the K-D-K) against the bench line's
+        # own algorithmic pass bytes (printed by the same command), per period
+        line = None
+        with open(f"{prof}/fetch.log") as fh:
+            for ln in fh:
+                if ln.startswith("{"):
+                    line = json.loads(ln)
+        periods = line["steps"] * (line["config"]["tf"] - 1)
+        alg = line["roofline"]["algorithmic_bytes_per_period"] * periods
+        hbm = 0.0
+        n = 0
+        for kname in ("dtc_kdk_pass", "dtc_kick_pass", "dtc_kick_swap_pass"):
+            fsel = fe[fe.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
+            wsel = wr[wr.Kernel_Name.str.contains(kname, regex=False)]["Counter_Value"]
+            hbm += 2 * fsel.sum() * 1024 + wsel.sum() * 1024
+            n += len(fsel)
+        res["lo_pass"] = {"kernel": "C5 pass kernels per period (dtc_kdk_pass, dtc_kick_pass, "
+                                    "dtc_kick_swap_pass)", "launches": n, "periods": periods,
+                          "hbm_bytes_per_launch": hbm / periods,
+                          "algorithmic_bytes_per_launch": alg / periods,
+                          "ratio_to_algorithmic": hbm / alg, "unit": "per period"}
+        with open(out, "w") as fh:
+            json.dump(res, fh, indent=1)
+        print(json.dumps(res, indent=1))
+        return
     # the K-D-K passes as the bench line aggregates them: dtc_kdk_pass /
     # dtc_kdk_pass3 (32 B per amplitude) and the dual forward+echo-start
     # dtc_kdk_dual (48 B: one read, two stores)
