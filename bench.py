@@ -1014,11 +1014,14 @@ def main_energy(args):
     sums = np.zeros((3, T, L))
 
     def step(i):
+        # the estimator's trajectory sums, reduced on the device (dtc_energy_sums:
+        # the same per-trajectory passes, a few KB instead of 15 MB of rows to
+        # the host per step)
         off = (rank * (args.warmup + args.steps) + i) * B
-        obs = eng.energy(spec, B, traj_offset=off, batch=B)
-        sums[0] += obs["z"][0].sum(axis=0)
-        sums[1, :, :L - 1] += obs["zz"][0].sum(axis=0)
-        sums[2] += obs["x"][0].sum(axis=0)
+        obs = eng.energy_sums(spec, B, traj_offset=off, batch=B)
+        sums[0] += obs["z"][0]
+        sums[1, :, :L - 1] += obs["zz"][0]
+        sums[2] += obs["x"][0]
 
     elapsed, acc, stats = _timed(eng, dist, args.warmup, args.steps, step, sums)
     if rank != 0:

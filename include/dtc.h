@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 10
+#define DTC_ABI_VERSION 11
 
 /* error codes */
 #define DTC_OK 0
@@ -298,6 +298,20 @@ int dtc_energy(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise, ui
 int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_noise* dv,
                       uint64_t seed, int64_t traj_offset, int32_t n_traj, double* z, double* zz,
                       double* x);
+
+/* The energy estimator's trajectory means without the per-trajectory rows
+ * (ABI 11): the same sweep as dtc_energy (dv == NULL) or dtc_energy_device
+ * (dv != NULL; noise unused then), reduced over the n_traj trajectories of
+ * each instance on the device:
+ *   z_sum  [n_inst][T][L], zz_sum [n_inst][T][L-1] (nullable when L = 1),
+ *   x_sum  [n_inst][T][L]
+ * = the sums over trajectories of dtc_energy's z, zz, x (fixed summation
+ * order; equal to the host sums of those rows up to rounding).  The energy
+ * scripts need only these means (energy.py:136-173: <H> from the estimator's
+ * expectation values); only a few KB per batch cross PCIe. */
+int dtc_energy_sums(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
+                    const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                    int32_t n_traj, double* z_sum, double* zz_sum, double* x_sum);
 
 /* Profiling: when enabled, every kernel launch is bracketed by HIP events on
  * the ctx stream and accumulated per kernel kind. */

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
 KERNEL_KINDS = 6  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass,
                   # virtual-rank exchange
-ABI_VERSION = 10  # DTC_ABI_VERSION of include/dtc.h this binding matches
+ABI_VERSION = 11  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "dtc_energy",
     "dtc_autocorr_device",
     "dtc_energy_device",
+    "dtc_energy_sums",
     "dtc_prefix_build",
     "dtc_autocorr_prefixed",
     "dtc_prefix_release",
@@ -227,6 +228,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         lib.dtc_energy_device.argtypes = [
             ctypes.c_void_p, P(DtcProblem), P(DtcDeviceNoise), ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_int32, _dp, _dp, _dp,
+        ]
+        lib.dtc_energy_sums.argtypes = [
+            ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcDeviceNoise), ctypes.c_uint64,
+            ctypes.c_int64, ctypes.c_int32, _dp, _dp, _dp,
         ]
         lib.dtc_prefix_build.argtypes = [
             ctypes.c_void_p, P(DtcProblem), P(DtcNoise), P(DtcDeviceNoise), ctypes.c_uint64,

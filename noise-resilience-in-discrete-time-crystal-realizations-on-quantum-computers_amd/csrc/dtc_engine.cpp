@@ -1956,9 +1956,11 @@ int dtc_apply_periods(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz, 
 
 namespace {
 
+// sums: z, zz, x are per-instance sums over the trajectories ([n_inst][T][.],
+// dtc_energy_sums) instead of per-trajectory rows
 int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                 const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset, int32_t n_traj,
-                double* z, double* zz, double* x) {
+                double* z, double* zz, double* x, bool sums = false) {
   if (!ctx || !z || !x || (!zz && pr && pr->L > 1)) return fail(DTC_EINVAL, "null ctx/outputs");
   DTC_TRY(check_problem(pr, nz));
   if (n_traj < 1) return fail(DTC_EINVAL, "n_traj must be >= 1");
@@ -2003,7 +2005,16 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   DTC_TRY(ensure(ctx->partial, (size_t)B * pl.n_tiles * n_obs * sizeof(double)));
   DTC_TRY(ensure(ctx->vals_f, (size_t)B * T * n_v * sizeof(double)));
   DTC_TRY(ensure(ctx->basis, (size_t)B * sizeof(int64_t)));
-  DTC_TRY(ensure_host(ctx->host_f, (size_t)B * T * n_v));
+  // per-instance sums: at most (B - 1) / n_traj + 2 instances per batch
+  const int64_t max_inst_b = std::min<int64_t>(pr->n_inst, (B - 1) / n_traj + 2);
+  if (sums) {
+    DTC_TRY(ensure(ctx->vals_e, (size_t)max_inst_b * T * n_v * sizeof(double)));
+    const size_t n_out = (size_t)pr->n_inst * T;
+    std::fill(z, z + n_out * L, 0.0);
+    std::fill(x, x + n_out * L, 0.0);
+    if (L > 1) std::fill(zz, zz + n_out * (L - 1), 0.0);
+  }
+  DTC_TRY(ensure_host(ctx->host_f, (size_t)(sums ? max_inst_b : B) * T * n_v));
   double* const hv_f = ctx->host_f.p;
   std::vector<int64_t> masks(B);
 
@@ -2138,6 +2149,49 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                                    vals + (size_t)e.t_mid * n_v + 2 * L, vs, 1, L, 1));
       }
     }
+    if (sums) {
+      // the batch's rows summed per instance on the device (the rows of the
+      // initial time are formed from the masks below, not read)
+      const int64_t i0 = bs / n_traj, n_ib = (bs + nb - 1) / n_traj - i0 + 1;
+      DTC_HIP(dtc::launch_traj_sum(vals, nb, (int)vs, bs, n_traj, (double*)ctx->vals_e.p,
+                                   ctx->stream));
+      DTC_HIP(hipMemcpyAsync(hv_f, ctx->vals_e.p, (size_t)n_ib * vs * sizeof(double),
+                             hipMemcpyDeviceToHost, ctx->stream));
+      DTC_HIP(hipStreamSynchronize(ctx->stream));
+      DTC_TRY(settle_pending(ctx));
+      for (int64_t i = 0; i < n_ib; ++i) {
+        const int64_t inst = i0 + i;
+        for (int t = 0; t < T; ++t) {
+          if (t + pr->t_offset == 0) continue;
+          const double* vf = hv_f + ((size_t)i * T + t) * n_v;
+          const double* vx = vf + 2 * L - 1;
+          double* zo = z + ((size_t)inst * T + t) * L;
+          double* xo = x + ((size_t)inst * T + t) * L;
+          for (int k = 0; k < L; ++k) {
+            zo[k] += vf[1 + k];
+            xo[k] += vx[1 + k];
+          }
+          if (L > 1) {
+            double* zzo = zz + ((size_t)inst * T + t) * (L - 1);
+            for (int k = 0; k + 1 < L; ++k) zzo[k] += vf[1 + L + k];
+          }
+        }
+      }
+      if (pr->t_offset == 0) {
+        for (int b = 0; b < nb; ++b) {
+          const int64_t inst = (bs + b) / n_traj;
+          const uint64_t m = (uint64_t)masks[b];
+          double* zo = z + (size_t)inst * T * L;
+          for (int k = 0; k < L; ++k) zo[k] += ((m >> k) & 1ull) ? -1.0 : 1.0;
+          if (L > 1) {
+            double* zzo = zz + (size_t)inst * T * (L - 1);
+            for (int k = 0; k + 1 < L; ++k)
+              zzo[k] += (((m >> k) ^ (m >> (k + 1))) & 1ull) ? -1.0 : 1.0;
+          }
+        }
+      }
+      continue;
+    }
     DTC_HIP(hipMemcpyAsync(hv_f, vals, (size_t)nb * T * n_v * sizeof(double),
                            hipMemcpyDeviceToHost, ctx->stream));
     DTC_HIP(hipStreamSynchronize(ctx->stream));
@@ -2180,6 +2234,17 @@ int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* pr, const dtc_device_nois
   if (!dv) return fail(DTC_EINVAL, "null device noise");
   const dtc_noise nz{0.0, 0, 0};
   return energy_impl(ctx, pr, &nz, dv, seed, traj_offset, n_traj, z, zz, x);
+}
+
+int dtc_energy_sums(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
+                    const dtc_device_noise* dv, uint64_t seed, int64_t traj_offset,
+                    int32_t n_traj, double* z_sum, double* zz_sum, double* x_sum) {
+  if (dv) {
+    const dtc_noise none{0.0, 0, 0};
+    return energy_impl(ctx, pr, &none, dv, seed, traj_offset, n_traj, z_sum, zz_sum, x_sum, true);
+  }
+  if (!nz) return fail(DTC_EINVAL, "null noise");
+  return energy_impl(ctx, pr, nz, nullptr, seed, traj_offset, n_traj, z_sum, zz_sum, x_sum, true);
 }
 
 int32_t dtc_plan_groups(int32_t n_bits, uint64_t* masks, int32_t max_groups) {

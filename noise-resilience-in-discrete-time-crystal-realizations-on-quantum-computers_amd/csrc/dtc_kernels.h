@@ -312,6 +312,12 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
                          int o_first = 0, int n_out = -1, int accumulate = 0,
                          double* scratch = nullptr);
 
+// Per-instance trajectory sums of a batch's per-state rows: vals [nb][cols],
+// state b of instance (batch_start + b) / n_traj; out [instances of the
+// batch, first = batch_start / n_traj][cols] (fixed summation order).
+hipError_t launch_traj_sum(const double* vals, int nb, int cols, int64_t batch_start, int n_traj,
+                           double* out, hipStream_t stream);
+
 // amplitude idx[b] of state b = 1 (after the caller zeroed the batch), in the
 // batch layout of octet_bits (state_base / octet_spread)
 hipError_t launch_set_basis(double2* state, int64_t state_len, const int64_t* idx,

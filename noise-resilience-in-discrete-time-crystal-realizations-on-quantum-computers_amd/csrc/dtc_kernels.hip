@@ -1342,6 +1342,39 @@ hipError_t launch_reduce(const double* partial, int n_tiles, int n_obs, int batc
   return hipGetLastError();
 }
 
+// Per-instance sums over the trajectories of a batch (dtc_energy_sums):
+// out[i][c] = sum over the states b of instance inst0 + i in this batch of
+// vals[b][c], c < cols; states b hold instance (batch_start + b) / n_traj.
+// One thread per column, states in a fixed order (four interleaved partial
+// sums, combined in order).
+__global__ __launch_bounds__(256) void traj_sum_kernel(const double* __restrict__ vals, int nb,
+                                                       int cols, int64_t batch_start, int n_traj,
+                                                       double* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t inst0 = batch_start / n_traj;
+  const int64_t inst = inst0 + blockIdx.y;
+  const int64_t lo0 = inst * n_traj - batch_start, hi0 = (inst + 1) * n_traj - batch_start;
+  const int64_t lo = lo0 > 0 ? lo0 : 0, hi = hi0 < nb ? hi0 : nb;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t b = lo;
+  for (; b + 3 < hi; b += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += vals[(b + u) * cols + c];
+  }
+  for (; b < hi; ++b) a[0] += vals[b * cols + c];
+  out[(int64_t)blockIdx.y * cols + c] = (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+hipError_t launch_traj_sum(const double* vals, int nb, int cols, int64_t batch_start, int n_traj,
+                           double* out, hipStream_t stream) {
+  if (nb < 1 || cols < 1 || n_traj < 1 || batch_start < 0) return hipErrorInvalidValue;
+  const int64_t n_inst = (batch_start + nb - 1) / n_traj - batch_start / n_traj + 1;
+  hipLaunchKernelGGL(traj_sum_kernel, dim3((cols + 255) / 256, (unsigned)n_inst), dim3(256), 0,
+                     stream, vals, nb, cols, batch_start, n_traj, out);
+  return hipGetLastError();
+}
+
 __global__ void set_basis_kernel(double2* state, int64_t state_len, const int64_t* idx,
                                  int batch, int og) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;

@@ -145,18 +145,20 @@ def get_instances_energy(spec: SweepSpec, n_traj: int = ESTIMATOR_SHOTS,
                          traj_offset: int = 0, readout=None) -> dict:
     """``get_instances`` of the energy scripts: ``<H>(t)`` per instance
     (``[inst][T]``) for each requested Hamiltonian variant, as the trajectory
-    mean of the engine's per-trajectory observables (``readout`` = per-site
-    (p01, p10) applied to them, device-like noise)."""
-    obs = _engine(engine).energy(spec, n_traj, seed=seed, traj_offset=traj_offset)
+    mean of the engine's observables (``readout`` = per-site (p01, p10)
+    applied to them, device-like noise).  <H> and the read-out map are affine
+    in the observables, so the means come from the engine's on-device
+    trajectory sums (``energy_sums``, dtc_energy_sums)."""
+    sums = _engine(engine).energy_sums(spec, n_traj, seed=seed, traj_offset=traj_offset)
+    obs = {k: v / n_traj for k, v in sums.items()}
     if readout is not None:
         obs = readout_observables(obs, *readout)
     out = {}
     for ht in hamiltonian_types:
-        per = np.stack([
+        out[ht] = np.stack([
             energy_from_observables({k: v[i] for k, v in obs.items()}, spec.L, _g0(spec.g),
                                     spec.hs[i], spec.phis[i], ht)
             for i in range(spec.n_inst)])
-        out[ht] = per.mean(axis=1)
     return out
 
 

@@ -284,6 +284,29 @@ class DtcEngine:
                 *outs))
         return {"z": z, "zz": zz, "x": x}
 
+    def energy_sums(self, spec: SweepSpec, n_traj: int, seed: int = 0x5EED0001,
+                    traj_offset: int = 0, batch: int = 0):
+        """``energy``'s observables summed over each instance's ``n_traj``
+        trajectories on the device (dtc_energy_sums; device-like noise when
+        ``spec.device`` is set): ``z`` [n_inst][T][L], ``zz`` [..][L-1], ``x``
+        [..][L].  Divide by ``n_traj`` for the estimator's means."""
+        n_inst, T, L = spec.n_inst, spec.T, spec.L
+        z = np.zeros((n_inst, T, L))
+        zz = np.zeros((n_inst, T, max(L - 1, 0)))
+        x = np.zeros((n_inst, T, L))
+        pr = self._problem(spec, True, False, batch, 0)
+        dv = None
+        if spec.device is not None:
+            if spec.device.L != spec.L:
+                raise ValueError("device noise has a different number of sites")
+            dv = _capi.device_struct(spec.device)
+        _capi.check(self._lib.dtc_energy_sums(
+            self._ctx, ctypes.byref(pr), ctypes.byref(self._noise(spec)),
+            ctypes.byref(dv) if dv is not None else None, ctypes.c_uint64(seed),
+            ctypes.c_int64(traj_offset), ctypes.c_int32(n_traj), _capi.as_dptr(z),
+            _capi.as_dptr(zz) if L > 1 else None, _capi.as_dptr(x)))
+        return {"z": z, "zz": zz, "x": x}
+
     # -- sharded state (dtc_shard_*; driver: sharded.py) ----------------
     def shard_set_basis(self, spec: SweepSpec, shard, state_ptr: int, seed: int = 0x5EED0001,
                         traj: int = 0):

@@ -16,3 +16,10 @@ def shot_sigma(a, shots=1024):
 def chi2_per_dof(x, y, sx, sy):
     r = (np.asarray(x) - np.asarray(y)) / np.sqrt(np.asarray(sx) ** 2 + np.asarray(sy) ** 2)
     return float(np.mean(r ** 2)), float(np.max(np.abs(r)))
+
+
+def harsh_device(pkg, L):
+    """A device-like noise model with strong damping (the device tests')."""
+    return pkg.DeviceNoise(p_gate=np.full(L, 0.02), t1_us=np.linspace(1.5, 3.0, L),
+                           t2_us=np.linspace(1.0, 4.0, L), gate_ns=120.0, anc_factor=0.9,
+                           readout_p01=0.02, readout_p10=0.035)

@@ -41,7 +41,7 @@ def test_library_is_gfx950_code_object(pkg):
 
 def test_abi_version_and_null_errors(pkg):
     lib = pkg._capi.load_library()
-    assert lib.dtc_abi_version() == 10 == pkg._capi.ABI_VERSION
+    assert lib.dtc_abi_version() == 11 == pkg._capi.ABI_VERSION
     # null context / arguments are rejected before any device call
     assert lib.dtc_autocorr(None, None, None, 0, 0, 1, None, None, None) == -1
     assert b"null" in lib.dtc_last_error()

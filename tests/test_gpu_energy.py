@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from oracle import dm_oracle, energy_oracle
-from tests.helpers import random_disorder
+from tests.helpers import harsh_device, random_disorder
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-10
@@ -134,3 +134,33 @@ def test_energy_neel_mean_vs_density_matrix(pkg, engine, L):
         v = got[key][0]
         mean, sd = v.mean(axis=0), v.std(axis=0) / np.sqrt(n) + 1e-12
         assert np.all(np.abs(mean - exact[k]) < 5 * sd), key
+
+
+@pytest.mark.parametrize("L,T,n_inst,n_traj,batch,state,toff,device", [
+    (5, 6, 2, 7, 0, "neel", 0, False),      # instances in one batch
+    (14, 5, 3, 5, 4, "vacuum", 0, False),    # batches that split instances
+    (20, 4, 1, 24, 16, "vacuum", 1, False),  # octet layout, t_offset = 1
+    (7, 5, 2, 6, 5, "neel", 0, True),        # device-like noise
+])
+def test_energy_sums_match_trajectory_rows(pkg, engine, L, T, n_inst, n_traj, batch, state, toff,
+                                           device):
+    """dtc_energy_sums (the per-instance trajectory sums on the device) equals
+    the host sums of dtc_energy's per-trajectory rows up to rounding, for any
+    batching, and get_instances_energy (which now uses it) equals the means of
+    those rows."""
+    rng = np.random.default_rng(L * 3 + n_traj)
+    hs, phis = random_disorder(rng, L, n_inst)
+    kw = {"device": harsh_device(pkg, L)} if device else {"noise_prob": 0.05}
+    spec = pkg.energy.energy_spec(L, T, hs, phis, 0.93, state, t_offset=toff, **kw)
+    rows = engine.energy(spec, n_traj, seed=44, traj_offset=3)
+    sums = engine.energy_sums(spec, n_traj, seed=44, traj_offset=3, batch=batch)
+    for key in ("z", "zz", "x"):
+        ref = rows[key].sum(axis=1)
+        assert sums[key].shape == ref.shape
+        assert np.abs(sums[key] - ref).max() < 1e-12 * n_traj, key
+    e = pkg.energy.get_instances_energy(spec, n_traj, seed=44, engine=engine, traj_offset=3)["full"]
+    means = {k: v.mean(axis=1) for k, v in rows.items()}
+    ref_e = np.stack([pkg.energy.energy_from_observables({k: v[i] for k, v in means.items()}, L,
+                                                         0.93, hs[i], phis[i], "full")
+                      for i in range(n_inst)])
+    assert np.abs(e - ref_e).max() < 1e-11
