@@ -239,26 +239,25 @@ __device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chun
 }
 
 // Value of lane (l ^ M) for every lane l, M = 1 .. 32, without LDS: DPP
-// quad permutes (1, 2), a row rotation (8) and a half-row mirror followed by a
-// quad reversal (4: lane l reads (l & 8) | (7 - (l ^ 3) & 7) = l ^ 4) on the
-// VALU, and gfx950's v_permlane16_swap / v_permlane32_swap (16, 32).  Every
-// DPP source lane is inside the row, so bound_ctrl with no old value: one
-// v_mov_b32_dpp per 32 bits (the old-value form cost a v_mov of 0 before
-// each).  permlane{16,32}_swap(x, x) returns (x with its even rows/lower half
-// copied up, x with its odd rows/upper half copied down): the xor partner is
-// the first for lanes with the bit set.
+// quad permutes (1, 2) and row rotations (4, 8) on the VALU, and gfx950's
+// v_permlane16_swap / v_permlane32_swap (16, 32).  A row rotation by n gives
+// lane l the value of lane ((l - n) mod 16); l ^ 8 is one such rotation, l ^ 4
+// is (l + 4) or (l - 4) by lane bit 2.  permlane{16,32}_swap(x, x) returns
+// (x with its even rows/lower half copied up, x with its odd rows/upper half
+// copied down): the xor partner is the first for lanes with the bit set.
 template <int M>
 __device__ __forceinline__ int xor_lane_b32(int x) {
   static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor");
   if constexpr (M == 1) {
-    return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   } else if constexpr (M == 2) {
-    return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
   } else if constexpr (M == 8) {
-    return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true);  // row_ror:8
+    return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
   } else if constexpr (M == 4) {
-    const int m = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);  // row_half_mirror
-    return __builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, true);          // quad_perm [3,2,1,0]
+    const int up = __builtin_amdgcn_update_dpp(0, x, 0x12C, 0xF, 0xF, false);  // l - 12 = l + 4
+    const int dn = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // l - 4
+    return (__lane_id() & 4) ? dn : up;
   } else if constexpr (M == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
     return (__lane_id() & 16) ? (int)r[0] : (int)r[1];
