@@ -223,6 +223,40 @@ __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_ha
   for (int r = 0; r < kRegs; ++r) v[r].y = s_half[DTC_SLOT(bt, TO, r)];
 }
 
+// Two tiles re-laid out together (the dual pass's forward and echo tiles),
+// each through its own half-tile buffer with the same slots: three barriers
+// for both.  Each buffer follows exchange_split's slot discipline.
+template <int FROM, int TO>
+__device__ __forceinline__ void exchange_split2(double2 (&v)[kRegs], double2 (&w)[kRegs],
+                                                double* s_a, double* s_b, int t) {
+  if (FROM == TO) return;
+  int bf = slot_add(ybase<FROM>(t)), bt = slot_add(ybase<TO>(t));
+  asm volatile("" : "+v"(bf), "+v"(bt));
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    s_a[DTC_SLOT(bf, FROM, r)] = v[r].x;
+    s_b[DTC_SLOT(bf, FROM, r)] = w[r].x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    v[r].x = s_a[DTC_SLOT(bt, TO, r)];
+    w[r].x = s_b[DTC_SLOT(bt, TO, r)];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    s_a[DTC_SLOT(bf, FROM, r)] = v[r].y;
+    s_b[DTC_SLOT(bf, FROM, r)] = w[r].y;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    v[r].y = s_a[DTC_SLOT(bt, TO, r)];
+    w[r].y = s_b[DTC_SLOT(bt, TO, r)];
+  }
+}
+
 template <bool SPLIT, int FROM, int TO>
 __device__ __forceinline__ void xch_tile(double2 (&v)[kRegs], double2* s_tile, double* s_half,
                                          int t) {

@@ -471,6 +471,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   DTC_TS(0);
   __shared__ double2 s_tile[SPLIT ? 1 : kTile];
   __shared__ double s_half[SPLIT ? kHalfSlots : 1];
+  // the co-traversed dual pass's second half-tile buffer (the echo's tile)
+  __shared__ double s_half2[(DUAL && SHAPE == kShapeKDK) ? kHalfSlots : 1];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
   __shared__ double s_red[kThreads / 64][kRedSlots];
@@ -918,10 +920,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     }
   }
   DTC_TS(3);
-  if constexpr (DUAL) {
+  // DUAL, unitary K-D-K: the echo branch's tile w runs its kick layer K'_1
+  // beside the forward's post-kick, nibble by nibble in the same order (O ->
+  // 0 -> IO), the two tiles re-laid out together through two half-tile
+  // buffers (three barriers per re-layout for both) and stored after the
+  // forward's tile: the pass makes the post-kick's re-layouts once, not twice
+  constexpr bool kCo = DUAL && RP::post && !kRho;
+  double2 w[DUAL ? kRegs : 1];
+  if constexpr (kCo) {
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) w[r] = v[r];
+  } else if constexpr (DUAL) {
     // the echo branch: E = K'_1 K_p (input) -- the forward pass's D, its
     // post-kick K_{p+1} and the echo's D^* and undo of K_{p+1} cancel exactly
-    double2 w[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
     // (device-like noise, a forward K-D: E = K'_1 D^* D K_p (input) -- the
@@ -973,7 +984,25 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // ---- post-kick rounds: 1 -> 0 -> 2 ----
   // (X before a nibble's post-kick: scale 1 / w_post^2 times prod w^2 of the
   // post nibbles already applied)
-  if constexpr (RP::post) {
+  if constexpr (kCo) {
+    static_assert(SPLIT, "co-traversed dual pass: half-tile re-layouts");
+    if constexpr (RP::nO) {
+      exchange_split2<RP::d_lay, RP::O>(v, w, s_half, s_half2, t);
+      apply_nibble<RP::O, KIND>(v, R, kTileBits);
+      apply_nibble<RP::O, KIND>(w, R2, kTileBits);
+    }
+    if constexpr (RP::n0) {
+      exchange_split2<RP::pO, 0>(v, w, s_half, s_half2, t);
+      apply_nibble<0, KIND>(v, R, kTileBits);
+      apply_nibble<0, KIND>(w, R2, kTileBits);
+    }
+    if constexpr (RP::nIO) {
+      exchange_split2<RP::p0, RP::IO>(v, w, s_half, s_half2, t);
+      apply_nibble<RP::IO, KIND>(v, R, kTileBits);
+      apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
+    }
+    exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t);
+  } else if constexpr (RP::post) {
     double sc = inv_w2_mid;
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::d_lay, RP::O>(v, s_tile, s_half, t);
@@ -1026,6 +1055,18 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       } else {
         *(double2*)a = v[r];
       }
+    }
+  }
+  if constexpr (kCo) {
+    // the echo branch's tile, after the forward's: its global factor i^k w
+    // of K_p and of K'_1
+    const double2 gE = make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1));
+    char* d2 = (char*)(A.dst2 + sbase);
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const double2 u = cmul(w[r], gE);
+      d2v x = {u.x, u.y};
+      __builtin_nontemporal_store(x, (d2v*)(d2 + tile_ofs(r) + (ofs32 ? (int64_t)vofs : vofs64)));
     }
   }
   if constexpr (MC == 1) {

@@ -9,6 +9,8 @@
 #   smoke              __graft_entry__.smoke()
 #   tests[:<expr>]     pytest -m gpu [-k <expr>] -> <tag>_gputest.txt
 #   ab:<VAR=v>,<VAR=v> interleaved env A/B of the C2 line under rocprof (tools/ab_env.sh)
+#   ablibs:<l1>,<l2>.. interleaved library A/B of the C2 line under rocprof (tools/ab_libs.sh;
+#                      "base" = the product library, else a devlib/*.so built in the container)
 #   stage              copy this call's PMC summaries (gpurun_out/<tag>*_pmc*.json) into
 #                      profiles/ of the box's copy, so later bench steps cite them
 #   exec:<file>        run gpu_bin/<file> (a probe built in the container) -> <tag>_<file>.txt
@@ -44,6 +46,9 @@ for step in "$@"; do
     ab:*)
       IFS=, read -ra settings <<< "${step#ab:}"
       bash tools/ab_env.sh $TAG "${settings[@]}" || exit 1 ;;
+    ablibs:*)
+      IFS=, read -ra libs <<< "${step#ablibs:}"
+      bash tools/ab_libs.sh $TAG "${libs[@]}" || exit 1 ;;
     stage)
       cp $O/${TAG}*_pmc*.json profiles/ || exit 1
       ls profiles/${TAG}*_pmc*.json ;;
