@@ -117,6 +117,25 @@ struct RecRegs {
   __device__ __forceinline__ int i(int rec, int e) const { return (int)bits(8 * rec + e); }
 };
 
+// The same records read through the scalar data cache instead: the block's
+// address is uniform, so with the constant address space every value is an
+// s_load into SGPRs (batched by the compiler) and a butterfly takes it as an
+// SGPR operand -- no v_readlane_b32 pair per value.  For the VALU-bound
+// light-cone ends (dtc_lcw3_final: 98 readlanes of 2818 VALU per wave).  The
+// records are written by an earlier kernel of the stream (prep_kernel); the
+// scalar cache is invalidated at every dispatch.
+struct RecScalar {
+  typedef __attribute__((address_space(4))) const long long* cptr;
+  cptr p;
+  __device__ __forceinline__ explicit RecScalar(const KickRec* rec)
+      : p((cptr)(const void*)rec) {}
+  __device__ __forceinline__ long long bits(int j) const { return p[j]; }
+  __device__ __forceinline__ double d(int rec, int e) const {
+    return __longlong_as_double(p[8 * rec + e]);
+  }
+  __device__ __forceinline__ int i(int rec, int e) const { return (int)p[8 * rec + e]; }
+};
+
 template <int N, int KIND>
 __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs& R, int rec0) {
   // Every site of an active nibble runs (inactive sites carry the identity):

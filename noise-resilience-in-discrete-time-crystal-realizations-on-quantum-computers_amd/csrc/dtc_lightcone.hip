@@ -50,17 +50,9 @@ __device__ __forceinline__ void lc_body(const PassArgs& A) {
   const int64_t tile0 = (og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x) * TPB;
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcPacked + 1) {  // the records: lanes 0 .. 10
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
+  // the state's records through the scalar data cache (RecScalar): these
+  // ends are VALU-bound, a v_readlane pair per coefficient is an issue slot
+  const RecScalar R(A.recs + b * kRecPerState);
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
   M.c = c;
@@ -284,17 +276,9 @@ __global__ __launch_bounds__(kThreads, 3) void dtc_lcw_final(PassArgs A) {
   const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcwMask + kLcwLayers) {  // the records: lanes 0 .. 19
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
+  // the state's records through the scalar data cache (RecScalar): these
+  // ends are VALU-bound, a v_readlane pair per coefficient is an issue slot
+  const RecScalar R(A.recs + b * kRecPerState);
   constexpr int kConePerThread = (kLcTab5b + 64 + kThreads - 1) / kThreads;
   double2 cv[kConePerThread];
   const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
@@ -634,17 +618,9 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   const int j = A.probe;
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcwMask + kLcwLayers) {  // the records: lanes 0 .. 19
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
+  // the state's records through the scalar data cache (RecScalar): these
+  // ends are VALU-bound, a v_readlane pair per coefficient is an issue slot
+  const RecScalar R(A.recs + b * kRecPerState);
   // global bit of each window site; the tile's base (its id deposited into
   // the bits off the window, as lc_merge_wide's lc_gb)
   auto gpos = [&](int s) { return s == c0 ? 0 : (s == c1 ? 1 : j + off_of(s)); };
@@ -972,17 +948,9 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   const int j = A.probe;
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < kLcw3Mask + kLcw3Layers) {  // the records: lanes 0 .. 22
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
+  // the state's records through the scalar data cache (RecScalar): these
+  // ends are VALU-bound, a v_readlane pair per coefficient is an issue slot
+  const RecScalar R(A.recs + b * kRecPerState);
   // global bit of each window site; the tile's base: its id in bits
   // 0 .. j-6 and j+7 .. (the host checks j >= 6: bit j-6 is an id bit)
   auto gpos = [&](int s) { return j + off_of(s); };
