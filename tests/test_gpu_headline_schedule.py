@@ -125,3 +125,37 @@ def test_headline_schedule_echo_only_and_t_first(pkg, engine, headline):
     _check(late, oracle, 0, t_first=20)
     assert not np.any(late["echo"][..., :20])
     engine.release_buffers()
+
+
+def test_c3_schedule_long_chains_match_oracle(pkg, engine):
+    """bench.py --config c3 (BASELINE configs[2]'s device-like noise on the C2
+    sweep: the stand-in calibration data/device_standin_L20.json, 1024
+    trajectories per launch, traj_offset = step * 1024), both first batches:
+    ids 7, 1023 and 1024 equal the gate-by-gate device oracle at 1e-10 on the
+    longest echo chains (t = 26..29, the oracle run with t_first = 26 to bound
+    its cost; the engine's values at t >= t_first do not depend on t_first),
+    fwd and echo.  Exercises the device dual pass (dtc_kd_dual) and the
+    kick-only ends at the line's own batch."""
+    _free_device_memory(engine)
+    spec = _spec(pkg)
+    cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data", "device_standin_L20.json"))
+    spec.device = cal.device_noise(20)
+    from concurrent.futures import ThreadPoolExecutor
+
+    ids = [7, 1023, 1024]
+
+    def one(g):  # one oracle trajectory per host thread (ctypes drops the GIL)
+        o = c_oracle.autocorr(spec, 1, seed=SEED, traj_offset=g, t_first=26)
+        return o["fwd"][0, 0], o["echo"][0, 0]
+
+    with ThreadPoolExecutor(len(ids)) as ex:
+        ref = dict(zip(ids, ex.map(one, ids)))
+    for off in (0, B):
+        got = engine.autocorr(spec, B, seed=SEED, traj_offset=off, batch=B)
+        for g in ids:
+            if not off <= g < off + B:
+                continue
+            for k, r in zip(("fwd", "echo"), ref[g]):
+                err = float(np.abs(got[k][0, g - off, 26:] - r[26:]).max())
+                assert err < TOL, (k, g, err)
+    engine.release_buffers()
