@@ -136,8 +136,8 @@ struct RecScalar {
   __device__ __forceinline__ int i(int rec, int e) const { return (int)p[8 * rec + e]; }
 };
 
-template <int N, int KIND>
-__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const RecRegs& R, int rec0) {
+template <int N, int KIND, typename Rec>
+__device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, int rec0) {
   // Every site of an active nibble runs (inactive sites carry the identity):
   // no data-dependent branches, so no register shuffles at merge points; the
   // RX/RY variant branch is wave-uniform.

@@ -489,29 +489,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
-  // this state's kick records (prep kernel), lane-distributed (RecRegs)
-  RecRegs R;
-  {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < 8 * kRecPerState) {
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R.rv[0] = r0.x; R.rv[1] = r0.y; R.rv[2] = r1.x; R.rv[3] = r1.y;
-  }
-  RecRegs R2;  // DUAL: the echo branch's records (its post-kick and total)
-  if constexpr (DUAL) {
-    const int lane = t & 63;
-    const double2* rp = (const double2*)(A.recs2 + b * kRecPerState) + 2 * lane;
-    double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
-    if (4 * lane < 8 * kRecPerState) {
-      r0 = rp[0];
-      r1 = rp[1];
-    }
-    R2.rv[0] = r0.x; R2.rv[1] = r0.y; R2.rv[2] = r1.x; R2.rv[3] = r1.y;
-  }
+  // this state's kick records (prep kernel), through the scalar data cache
+  // (RecScalar: uniform s_loads into SGPRs)
+  const RecScalar R(A.recs + b * kRecPerState);
+  // DUAL: the echo branch's records (its post-kick and total)
+  const RecScalar R2(DUAL ? A.recs2 + b * kRecPerState : A.recs + b * kRecPerState);
 
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
@@ -864,7 +846,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // device-like noise: a kick layer's deferred Kraus factors (SiteMat),
   // prod over the tile bits k of rho_{k, x_k}, in layout LAY (records rec0 ..)
   constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
-  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const RecRegs& Rr) {
+  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const RecScalar& Rr) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int y = ybase<LAY>(t);
     double rt = 1.0;
