@@ -1626,10 +1626,20 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     const bool lc_enabled = ctx->lightcone;
     // Forward chain K_1 D K_2 D ... K_P D; after each D_p: measure t = p - t_offset
     // and branch the echo at t off F.  The whole batch schedule is built first.
+    // Device-like noise (r5): the forward runs one kick layer ahead, one pass
+    // per period as in the unitary case, when every echo chain's first pass
+    // folds into the forward's dual pass -- the chain's echo start is then
+    // taken before that layer, so the layer (a Kraus kick, not invertible) is
+    // never undone; if any chain does not fold, the schedule is rebuilt with
+    // K-D forward passes (two passes per period, nothing run ahead).
     std::vector<Launch> sched;
+    for (bool dev_ahead = rc.device && ctx->dual;;) {
+    sched.clear();
+    bool all_folded = true;
+    const bool dev_kd = rc.device && !dev_ahead;  // device-like noise, K-D forward
     if (P > n_pre) {
       Chain fw = forward_chain(pl, n_pre + 1, P - n_pre, dtc::kStreamForward);
-      fw.post_after_d = !rc.device;
+      fw.post_after_d = !dev_kd;
       // start on a group without the probe site: every echo chain then ends
       // with its kick-only pass on such a group, which the probe does not need
       // (two groups: the closing groups alternate with p, see below)
@@ -1703,17 +1713,17 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         if (ctx->dual && sched.size() - chain0 >= 2 && chain0 >= 1) {
           Launch& f = sched[chain0 - 1];
           const Launch& e = sched[chain0];
-          const int fs = rc.device ? dtc::kShapeKD : dtc::kShapeKDK;
-          const int es = rc.device ? dtc::kShapeDK : dtc::kShapeKDK;
+          const int fs = dev_kd ? dtc::kShapeKD : dtc::kShapeKDK;
+          const int es = dev_kd ? dtc::kShapeDK : dtc::kShapeKDK;
           // (the dual kernels carry the probe at most: not with per-site Z)
           const bool fok = pass_shape(f.ps) == fs && !f.basis && f.src == F &&
                            (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
           const bool eok =
               pass_shape(e.ps) == es && e.ps.lc_w0 < 0 && e.ps.group == f.ps.group &&
               e.ps.post.enabled &&
-              (rc.device ? e.ps.post.skip == 0 && f.ps.pre.skip == 0
-                         : e.ps.pre.mode == dtc::kKickUndo && e.ps.pre.skip == 0 &&
-                               f.ps.post.skip == 0);
+              (dev_kd ? e.ps.post.skip == 0 && f.ps.pre.skip == 0
+                      : e.ps.pre.mode == dtc::kKickUndo && e.ps.pre.skip == 0 &&
+                            f.ps.post.skip == 0);
           // the fold is exact only when the chain's first pass conjugates the
           // forward's diagonal (one table per instance; d_index only counts
           // each chain's own periods) and, in the unitary case, undoes exactly
@@ -1721,7 +1731,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
           // falls back to the separate passes instead of folding wrongly
           const bool same_d = f.ps.diag == dtc::kDiagFwd && e.ps.diag == dtc::kDiagConj;
           const bool undoes_post =
-              rc.device || (f.ps.post.enabled && f.ps.post.mode == dtc::kKickForward &&
+              dev_kd || (f.ps.post.enabled && f.ps.post.mode == dtc::kKickForward &&
                             e.ps.pre.row == f.ps.post.row &&
                             e.ps.pre.stream == f.ps.post.stream &&
                             e.ps.pre.rng_period == f.ps.post.rng_period);
@@ -1731,14 +1741,24 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                                          : (fk == dtc::kKindRX || fk == dtc::kKindRY ||
                                             fk == dtc::kKindGen);
           const PassSpec branch{f.ps.group, f.ps.pre, e.ps.post, dtc::kDiagNone, 0};
-          if (fok && eok && kind_ok && fk == pass_kind(rc, e.ps, es) &&
+          // (run ahead under device-like noise, the chain's first pass holds an
+          // undo of a Kraus kick: its own kind is not a factored one, and it
+          // never runs)
+          if (fok && eok && kind_ok && (dev_ahead || fk == pass_kind(rc, e.ps, es)) &&
               fk == pass_kind(rc, branch, -1)) {
             f.ps2 = branch;
             f.dst2 = E;
             sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
+          } else {
+            all_folded = false;
           }
+        } else {
+          all_folded = false;
         }
       }
+    }
+    if (!dev_ahead || all_folded) break;
+    dev_ahead = false;
     }
     if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));

@@ -459,10 +459,11 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
   static_assert(!DUAL || (MC <= 1 && !NS &&
                           ((SHAPE == kShapeKDK &&
-                            (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) ||
+                            (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen ||
+                             KIND == kKindRXU || KIND == kKindRYU)) ||
                            (SHAPE == kShapeKD &&
                             (KIND == kKindRXU || KIND == kKindRYU || KIND == kKindGen)))),
-                "dual passes: unitary K-D-K or device-noise K-D, at most the probe");
+                "dual passes: K-D-K or device-noise K-D, at most the probe");
   constexpr int kNt = NIBS == 7 ? DTC_NT_A : DTC_NT_B;
 #ifdef DTC_PHASE_TIMING
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -906,12 +907,17 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // beside the forward's post-kick, nibble by nibble in the same order (O ->
   // 0 -> IO), the two tiles re-laid out together through two half-tile
   // buffers (three barriers per re-layout for both) and stored after the
-  // forward's tile: the pass makes the post-kick's re-layouts once, not twice
-  constexpr bool kCo = DUAL && RP::post && !kRho;
+  // forward's tile: the pass makes the post-kick's re-layouts once, not twice.
+  // Device-like noise (the forward running one layer ahead, r5: the echo's
+  // start is taken before that layer, so it is never undone): both tiles take
+  // the pre-kick's deferred Kraus diagonal here, each its own post-kick's
+  // before the stores.
+  constexpr bool kCo = DUAL && RP::post;
   double2 w[DUAL ? kRegs : 1];
   if constexpr (kCo) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
+    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
   } else if constexpr (DUAL) {
     // the echo branch: E = K'_1 K_p (input) -- the forward pass's D, its
     // post-kick K_{p+1} and the echo's D^* and undo of K_{p+1} cancel exactly
@@ -984,6 +990,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
     }
     exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t);
+    if constexpr (kRho) {
+      rho_apply(LIO{}, kTileBits, v, R);
+      rho_apply(LIO{}, kTileBits, w, R2);
+    }
   } else if constexpr (RP::post) {
     double sc = inv_w2_mid;
     if constexpr (RP::nO) {
@@ -1201,7 +1211,7 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
   }
   if (a.dst2) {
     // K-D-K: unitary kicks; K-D: device-like noise (factored or general kicks)
-    if constexpr (MC <= 1 && (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen)) {
+    if constexpr (MC <= 1) {
       if (shape == kShapeKDK) {
         hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
         return hipGetLastError();

@@ -244,13 +244,14 @@ def test_energy_cli_use_fakebackend(pkg, golden, tmp_path):
     (21, 4, "neel", "circular_left", 0),  # general 2x2 kicks (no factored form)
 ])
 def test_device_dual_pass(pkg, monkeypatch, L, T, state, pol, toff):
-    """Device-like noise runs no forward layer ahead, so a period closes with a
-    forward K-D on group G and the echo chain at that time starts with D^* K'_1
-    on G: dtc_kd_dual forms K'_1 K_p (input) from the K-D's tile after its
-    pre-kick (Kraus diagonals of both layers applied) and stores it to E.  Per
-    trajectory: the oracle's values (1e-10), the unfused schedule's
-    (DTC_NO_DUAL) to 1e-12, and one pass fewer per echo chain, factored or
-    general kicks."""
+    """Device-like noise with the dual pass: the forward runs one kick layer
+    ahead (one K-D-K pass per period) and every echo chain's first pass folds
+    into it -- dtc_kdk_dual forms K'_1 K_p (input) from the pass's tile after
+    its pre-kick (Kraus diagonals of both layers applied) and stores it to E,
+    so the run-ahead Kraus layer is never undone.  Without the dual pass
+    (DTC_NO_DUAL) nothing runs ahead: K-D forward passes, two per period.  Per
+    trajectory: the oracle's values (1e-10), the other schedule's to 1e-12,
+    and fewer passes, factored or general kicks."""
     rng = np.random.default_rng(L * 3 + T)
     hs, phis = random_disorder(rng, L, 2)
     spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, polarization=pol,
