@@ -249,7 +249,10 @@ def test_echo_light_cone_end(pkg, monkeypatch, L, T, p, state, pol, toff, probe,
     full, n_full = run(["DTC_NO_LIGHTCONE", "DTC_NO_DUAL"])
     for o in (single, narrow, full):
         assert np.abs(got["echo"] - o["echo"]).max() < 1e-12
-        assert np.abs(got["fwd"] - o["fwd"]).max() == 0.0
+        # (these run without the dual pass, whose forward tile shares its
+        # kernel with the echo's: the compiler may contract its FMAs
+        # differently, 1e-17 here, as in test_dual_pass_echo_start)
+        assert np.abs(got["fwd"] - o["fwd"]).max() < 1e-13
     assert n_wide <= n_narrow <= n_full
     if pol in ("x", "y"):  # factored kicks (general 2x2 kicks keep the full passes)
         assert n_narrow < n_full
