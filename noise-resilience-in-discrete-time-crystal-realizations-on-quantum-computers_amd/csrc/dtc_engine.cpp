@@ -1661,6 +1661,11 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
         std::vector<int> ahead(pl.groups.size());
         for (size_t g = 0; g < pl.groups.size(); ++g) ahead[g] = fw.kc[g] > ps.d_index;
         Chain ec = echo_chain(pl, p, (uint32_t)(1 + t), ahead);
+        // run ahead under device-like noise, a chain whose first pass undoes
+        // the forward's run-ahead layer must fold (the undo of a Kraus kick
+        // cannot run); the sweep's last chain, after a K-D, has none
+        bool must_fold = false;
+        for (size_t g = 0; g < pl.groups.size(); ++g) must_fold |= dev_ahead && ahead[g];
         if (rc.device && ctx->dual) {
           // device-like noise: the chain starts on the group whose forward
           // K-D closed the period (the dual pass below)
@@ -1749,10 +1754,10 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
             f.ps2 = branch;
             f.dst2 = E;
             sched.erase(sched.begin() + (std::ptrdiff_t)chain0);
-          } else {
+          } else if (must_fold) {
             all_folded = false;
           }
-        } else {
+        } else if (must_fold) {
           all_folded = false;
         }
       }

@@ -490,11 +490,32 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
-  // this state's kick records (prep kernel), through the scalar data cache
-  // (RecScalar: uniform s_loads into SGPRs)
-  const RecScalar R(A.recs + b * kRecPerState);
+  // this state's kick records (prep kernel): lane-distributed in VGPRs
+  // (RecRegs), loaded with the setup; the energy passes (MC 3) read them
+  // through the scalar data cache instead (RecScalar: the 24 X pair sums
+  // leave no VGPRs for them at three workgroups per CU -- r5f: their spill
+  // gone, pass3<7,0,3> 7.04 -> 6.90 ms; in the other passes the scalar loads
+  // sit on the tile's chain, kdk3<7,0,0> 5.34 -> 6.11 ms)
+  constexpr bool kScalarRec = MC == 3;
+  auto load_recs = [&](const KickRec* rec) {
+    if constexpr (kScalarRec) {
+      return RecScalar(rec);
+    } else {
+      RecRegs r;
+      const int lane = t & 63;
+      const double2* rp = (const double2*)rec + 2 * lane;
+      double2 r0 = make_double2(0.0, 0.0), r1 = make_double2(0.0, 0.0);
+      if (4 * lane < 8 * kRecPerState) {
+        r0 = rp[0];
+        r1 = rp[1];
+      }
+      r.rv[0] = r0.x; r.rv[1] = r0.y; r.rv[2] = r1.x; r.rv[3] = r1.y;
+      return r;
+    }
+  };
+  const auto R = load_recs(A.recs + b * kRecPerState);
   // DUAL: the echo branch's records (its post-kick and total)
-  const RecScalar R2(DUAL ? A.recs2 + b * kRecPerState : A.recs + b * kRecPerState);
+  const auto R2 = load_recs(DUAL ? A.recs2 + b * kRecPerState : A.recs + b * kRecPerState);
 
   const int64_t mid_mask = ((int64_t)1 << A.tile_bits_mid) - 1;
   TileMap M;
@@ -847,7 +868,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // device-like noise: a kick layer's deferred Kraus factors (SiteMat),
   // prod over the tile bits k of rho_{k, x_k}, in layout LAY (records rec0 ..)
   constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
-  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const RecScalar& Rr) {
+  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const auto& Rr) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int y = ybase<LAY>(t);
     double rt = 1.0;
