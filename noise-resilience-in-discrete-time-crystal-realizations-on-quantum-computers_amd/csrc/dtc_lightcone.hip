@@ -1018,35 +1018,77 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
     int64_t spq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) spq[q] = octet_spread((int64_t)1 << gpos(lay_site(kX1, q)), og) << 4;
+    // uniform base + one 32-bit lane offset (global_load with an SGPR base:
+    // no 64-bit address add per load) while the lane bits' byte offsets fit
+    const bool vofs32 = vofs < ((int64_t)1 << 32);
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
       int64_t o = sp0;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if ((r >> q) & 1) o += spq[q];
-      const d2v w = *(const d2v*)(src + o + vofs);
+      const d2v w = vofs32 ? *(const d2v*)(src + o + (uint32_t)vofs) : *(const d2v*)(src + o + vofs);
       v[r] = make_double2(w.x, w.y);
     }
   }
   // the cone-table entries this thread stages (e = t, t + 256 of the 456):
-  // loaded behind the tile, staged after the first layer
+  // loaded behind the tile, staged after the first layer.  Wave w's entries t
+  // lie in one table (6a, 6b, 6b, 5a) and its entries t + 256 in at most
+  // three (5b | 4a 4b | 3a 3b 2 | 1): the wave index is made uniform, so each
+  // wave runs only its own tables' index arithmetic (compile-time offsets,
+  // bit counts and layers), with lane selects where a wave spans two or three
   const double2* ct = A.lc_diag + (int64_t)inst * kLcTab;
-  auto tab_of = [](int e) {
-    return e >= tab_off(kT1) ? kT1 : e >= tab_off(kT2) ? kT2 : e >= tab_off(kT3b) ? kT3b
-         : e >= tab_off(kT3a) ? kT3a : e >= tab_off(kT4b) ? kT4b : e >= tab_off(kT4a) ? kT4a
-         : e >= tab_off(kT5b) ? kT5b : e >= tab_off(kT5a) ? kT5a : e >= tab_off(kT6b) ? kT6b : kT6a;
+  // entry i of table K in the instance's tables (6a: the workgroup's bit j-6
+  // is index bit 0 there; 5a is stored lc_pos5a-swizzled) and its staged slot
+  // (i ^ m_K, m_K the frame's X mask after the table's layer on its bits)
+  auto src_of = [&](auto k_tag, int i) {
+    constexpr int K = decltype(k_tag)::value;
+    return tab_src(K) + (K == kT6a ? ((i << 1) | b6) : K == kT5a ? lc_pos5a(i) : i);
   };
-  // entry i of table k in the instance's tables (6a: the workgroup's bit j-6
-  // is index bit 0 there; 5a is stored lc_pos5a-swizzled)
-  auto src_index = [&](int k, int i) {
-    return tab_src(k) + (k == kT6a ? ((i << 1) | b6) : k == kT5a ? lc_pos5a(i) : i);
+  auto dst_of = [&](auto k_tag, int i) {
+    constexpr int K = decltype(k_tag)::value;
+    const uint64_t m = (uint64_t)R.bits(kLcw3Mask + tab_layer(K));
+    return tab_off(K) + (i ^ (int)((m >> (j + tab_lo(K))) & ((1u << tab_bits(K)) - 1u)));
   };
-  const int e1 = t + kThreads;
-  const int k0 = tab_of(t), k1 = e1 < kTabEntries ? tab_of(e1) : kT1;
-  const int i0 = t - tab_off(k0), i1 = e1 - tab_off(k1);
-  const double2 tv0 = ct[src_index(k0, i0)];
+  using K6a = std::integral_constant<int, kT6a>;
+  using K6b = std::integral_constant<int, kT6b>;
+  using K5a = std::integral_constant<int, kT5a>;
+  using K5b = std::integral_constant<int, kT5b>;
+  using K4a = std::integral_constant<int, kT4a>;
+  using K4b = std::integral_constant<int, kT4b>;
+  using K3a = std::integral_constant<int, kT3a>;
+  using K3b = std::integral_constant<int, kT3b>;
+  using K2 = std::integral_constant<int, kT2>;
+  using K1 = std::integral_constant<int, kT1>;
+  static_assert(tab_off(kT6b) == 64 && tab_off(kT5a) == 192 && tab_off(kT5b) == 256 &&
+                    tab_off(kT4a) == 320 && tab_off(kT4b) == 352 && tab_off(kT3a) == 384 &&
+                    tab_off(kT3b) == 400 && tab_off(kT2) == 416 && tab_off(kT1) == 448 &&
+                    kTabEntries == 456 && kThreads == 256,
+                "the per-wave table split below");
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+  int s0, d0, s1 = -1, d1 = 0;
+  if (wv == 0) {
+    s0 = src_of(K6a{}, ln); d0 = dst_of(K6a{}, ln);
+    s1 = src_of(K5b{}, ln); d1 = dst_of(K5b{}, ln);
+  } else if (wv == 1) {
+    s0 = src_of(K6b{}, ln); d0 = dst_of(K6b{}, ln);
+    const bool a = ln < 32;
+    s1 = a ? src_of(K4a{}, ln) : src_of(K4b{}, ln - 32);
+    d1 = a ? dst_of(K4a{}, ln) : dst_of(K4b{}, ln - 32);
+  } else if (wv == 2) {
+    s0 = src_of(K6b{}, 64 + ln); d0 = dst_of(K6b{}, 64 + ln);
+    s1 = ln < 16 ? src_of(K3a{}, ln) : ln < 32 ? src_of(K3b{}, ln - 16) : src_of(K2{}, ln - 32);
+    d1 = ln < 16 ? dst_of(K3a{}, ln) : ln < 32 ? dst_of(K3b{}, ln - 16) : dst_of(K2{}, ln - 32);
+  } else {
+    s0 = src_of(K5a{}, ln); d0 = dst_of(K5a{}, ln);
+    if (ln < 8) {
+      s1 = src_of(K1{}, ln);
+      d1 = dst_of(K1{}, ln);
+    }
+  }
+  const double2 tv0 = ct[s0];
   double2 tv1 = make_double2(0.0, 0.0);
-  if (e1 < kTabEntries) tv1 = ct[src_index(k1, i1)];
+  if (s1 >= 0) tv1 = ct[s1];
   // ---- X1: l0 on p3 p4 p5 p6, p2 (swapped in) ----
   kick(C0{}, C0{}, LCW3_S(p3));
   kick(C1{}, C0{}, LCW3_S(p4));
@@ -1054,21 +1096,11 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
   kick(C3{}, C0{}, LCW3_S(p6));
   swap_reg_lane<3, 16>(v);  // register bit 3: p2 (lane bit 4: p6)
   kick(C3{}, C0{}, LCW3_S(p2));
-  // stage the tables: entry i of table k at i ^ m_k, m_k the frame's X mask
-  // after the table's layer on the table's bits; conjugated for D*
+  // stage the tables at their frame-masked slots, conjugated for D*
   {
     const double cs = A.diag_conj ? -1.0 : 1.0;
-    const uint64_t mm0 = (uint64_t)R.bits(kLcw3Mask + 0), mm1 = (uint64_t)R.bits(kLcw3Mask + 1);
-    const uint64_t mm2 = (uint64_t)R.bits(kLcw3Mask + 2), mm3 = (uint64_t)R.bits(kLcw3Mask + 3);
-    const uint64_t mm4 = (uint64_t)R.bits(kLcw3Mask + 4), mm5 = (uint64_t)R.bits(kLcw3Mask + 5);
-    auto stage = [&](int k, int i, double2 tv) {
-      const int l = tab_layer(k);
-      const uint64_t m = l == 0 ? mm0 : l == 1 ? mm1 : l == 2 ? mm2 : l == 3 ? mm3 : l == 4 ? mm4 : mm5;
-      const int x = i ^ (int)((m >> (j + tab_lo(k))) & ((1u << tab_bits(k)) - 1u));
-      s_tab[tab_off(k) + x] = make_double2(tv.x, cs * tv.y);
-    };
-    stage(k0, i0, tv0);
-    if (e1 < kTabEntries) stage(k1, i1, tv1);
+    s_tab[d0] = make_double2(tv0.x, cs * tv0.y);
+    if (s1 >= 0) s_tab[d1] = make_double2(tv1.x, cs * tv1.y);
   }
   __syncthreads();  // the tables, before D6 (the first re-layout comes later)
   // ---- D6 in X1e, l1 on p3 p4 p5 p2, m5 (swapped in) ----
