@@ -6,6 +6,7 @@
 #   bench:<cfg>        bench.py --config <cfg> line -> gpurun_out/<tag>_<cfg>_bench.json
 #   trace:<cfg>        the same command under rocprofv3 --kernel-trace --stats -> prof_<tag>_<cfg>/
 #   pmc:<cfg>:<B>[:L]  FETCH_SIZE / WRITE_SIZE passes at batch B -> <tag>_pmc_<cfg>.json
+#                      (c2: <tag>_pmc.json, the headline line's)
 #   smoke              __graft_entry__.smoke()
 #   tests[:<expr>]     pytest -m gpu [-k <expr>] -> <tag>_gputest.txt
 #   ab:<VAR=v>,<VAR=v> interleaved env A/B of the C2 line under rocprof (tools/ab_env.sh)
@@ -34,7 +35,11 @@ for step in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_${TAG}_$c -o kt -- python $R/bench.py --config $c --no-cpu-baseline --steps 2 --warmup 1 > $R/$O/prof_${TAG}_$c.log 2>&1) || { echo "$c trace failed"; tail -5 $O/prof_${TAG}_$c.log; exit 1; } ;;
     pmc:*)
       IFS=: read -r _ c b l <<< "$step"
-      L=${l:-20} BENCH_ARGS="--config $c" SUFFIX=_pmc_$c bash tools/pmc_traffic.sh $TAG $b || exit 1 ;;
+      if [ "$c" = c2 ]; then  # the headline line reads <tag>_pmc.json
+        L=${l:-20} BENCH_ARGS="" SUFFIX=_pmc bash tools/pmc_traffic.sh $TAG $b || exit 1
+      else
+        L=${l:-20} BENCH_ARGS="--config $c" SUFFIX=_pmc_$c bash tools/pmc_traffic.sh $TAG $b || exit 1
+      fi ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/${TAG}_smoke.txt 2>&1 || { cat $O/${TAG}_smoke.txt; exit 1; }
       tail -1 $O/${TAG}_smoke.txt ;;
