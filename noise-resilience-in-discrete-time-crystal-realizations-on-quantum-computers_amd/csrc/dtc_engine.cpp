@@ -771,9 +771,15 @@ int basis_source(dtc_ctx* ctx, std::vector<LaunchT>& sched, double2* F, int64_t 
 // the memory budget (per_state bytes each), the octet layout (dtc_kernels.h)
 // when a batch holds at least one octet; then B is a multiple of 8 unless one
 // batch takes every state.
-void batch_layout(const dtc_ctx* ctx, int64_t S, int64_t& B, int& octet) {
+// Batch size and state layout.  The octet layout (eight states interleaved
+// at 2^octet_bits amplitudes, one state per XCD) serves states below 1 GiB;
+// larger states (L_eff >= 26: C4) stay contiguous, the pass kernels then
+// giving each XCD an eighth of a state's tiles (r5r: C4 +3.5 %, the top
+// 8-site group's rows 16 MiB apart instead of 128 MiB)
+constexpr int kOctetMaxLeff = 25;
+void batch_layout(const dtc_ctx* ctx, int L_eff, int64_t S, int64_t& B, int& octet) {
   B = std::min<int64_t>(std::min<int64_t>(B, S), 65535);
-  octet = (ctx->octet_bits > 0 && B >= 8) ? ctx->octet_bits : 0;
+  octet = (ctx->octet_bits > 0 && B >= 8 && L_eff <= kOctetMaxLeff) ? ctx->octet_bits : 0;
   if (octet && B < S) B &= ~(int64_t)7;
 }
 
@@ -1567,7 +1573,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     B = std::max<int64_t>(1, std::min<int64_t>(B, 4096));
   }
   int octet = 0;
-  batch_layout(ctx, S, B, octet);
+  batch_layout(ctx, rc.pl.L_eff, S, B, octet);
   if (use_prefix) {
     // the prefix's states are in the layout they were built in
     octet = ctx->prefix_octet;
@@ -1831,7 +1837,7 @@ int prefix_build_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
   // there is an octet; autocorr_prefixed reads them in this layout
   int64_t B = 4096;
   int octet = 0;
-  batch_layout(ctx, S, B, octet);
+  batch_layout(ctx, pl.L_eff, S, B, octet);
   rc.octet_bits = octet;
   DTC_TRY(ensure(ctx->prefix, (size_t)dtc::octet_padded(S, octet) * pl.len * 16));
   ctx->prefix_masks.resize(S);
@@ -2022,7 +2028,7 @@ int energy_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
                                                4096));
   }
   int octet = 0;
-  batch_layout(ctx, S, B, octet);
+  batch_layout(ctx, rc.pl.L_eff, S, B, octet);
   rc.octet_bits = octet;
   const int64_t Bp = dtc::octet_padded(B, octet);
   DTC_TRY(ensure(ctx->F, (size_t)(Bp * pl.len * 16)));

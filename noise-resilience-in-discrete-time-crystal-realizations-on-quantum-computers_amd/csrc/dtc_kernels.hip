@@ -477,6 +477,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
   __shared__ double s_red[kThreads / 64][kRedSlots];
+  // three-per-CU energy passes: per wave, X point (post, pre), nibble, the
+  // eight lane partials of the nibble's four sites (x_now)
+  __shared__ double s_xpart[(SPLIT && MC == 3) ? kThreads / 64 : 1][2][3][32];
 
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;
@@ -487,7 +490,12 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // last partial octet leave at once (the whole workgroup)
   const int og = A.octet_bits;
   const int64_t b = og ? (((int64_t)blockIdx.y << 3) | (blockIdx.x & 7)) : (int64_t)blockIdx.y;
-  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  // contiguous states (large L, C4 / C5): blocks go round-robin over the 8
+  // XCDs, so XCD x takes the x-th eighth of the tiles, consecutive ones on one
+  // XCD (r5q: the top 8-site group's pass at L=28, rows 16 MiB apart)
+  const int64_t tile = og ? (int64_t)(blockIdx.x >> 3)
+                          : ((gridDim.x & 7) ? (int64_t)blockIdx.x
+                                             : (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
   if (og && b >= A.batch) return;
   const int inst = (int)((A.batch_start + b) / A.n_traj);
   // this state's kick records (prep kernel): lane-distributed in VGPRs
@@ -835,13 +843,24 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // per point and read after the stores' barrier as in the deferred form)
   double xpost[SPLIT ? 1 : 3][4];
   double xpre[SPLIT ? 1 : 3][4];
+  // (three per CU: each X point's four per-thread sums are reduced over lane
+  // bits 5, 4 (permlane swaps) and 3 (one DPP row rotation) only, and the
+  // eight partials per site left in lanes 0..7 of each 16 go to LDS (s_xpart);
+  // x_combine adds them after the stores, off the tile's chain)
   auto x_now = [&](auto lay_tag, double scale, int slot0) {
     constexpr int LAY = decltype(lay_tag)::value;
     double a[4];
     pair_sums(lay_tag, a, scale);
-    const double k = wave_sum_multi<4>(a);
+    double u0 = a[0], w0 = a[2], u1 = a[1], w1 = a[3];
+    swap_rows<32>(u0, w0);
+    swap_rows<32>(u1, w1);
+    double b0 = u0 + w0, b1 = u1 + w1;
+    swap_rows<16>(b0, b1);
+    double cc = b0 + b1;
+    cc += xor_lane<8>(cc);
     const int lane = t & 63;
-    if ((lane & 15) == 0) s_red[t >> 6][slot0 + 4 * LAY + (lane >> 4)] = k;
+    const int pt = slot0 == kSlotXPre ? 1 : 0;
+    if (!(lane & 8)) s_xpart[t >> 6][pt][LAY][((lane >> 4) << 3) | (lane & 7)] = cc;
   };
   auto measure_x_post = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
@@ -1119,8 +1138,16 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
       double acc = 0.0;
       if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
-        const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
-        for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
+        if constexpr (SPLIT) {
+          const double* px = &s_xpart[0][pre ? 1 : 0][tb >> 2][(tb & 3) << 3];
+          constexpr int kW = 2 * 3 * 32;  // doubles per wave
+          for (int w = 0; w < kThreads / 64; ++w)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc += px[w * kW + i];
+        } else {
+          const int slot = (pre ? kSlotXPre : kSlotXPost) + tb;
+          for (int w = 0; w < kThreads / 64; ++w) acc += s_red[w][slot];
+        }
       }
       A.partial[(b * n_tiles + tile) * A.n_obs + 2 * L + xo] = acc;
     };
