@@ -109,10 +109,13 @@ def test_noiseless_L20_statevector_oracle(pkg, engine, golden):
     np.testing.assert_allclose(out["echo"][0, 0], np.ones(10), atol=1e-10)
 
 
-def test_batching_and_sharding_invariance(pkg, engine):
-    """Per-trajectory values depend only on the global trajectory id."""
+@pytest.mark.parametrize("L", [14, 16])
+def test_batching_and_sharding_invariance(pkg, engine, L):
+    """Per-trajectory values depend only on the global trajectory id.  The full
+    batch (12 states) runs in the octet layout, batches of 1 and 5 in the
+    contiguous one; at L=16 (16 tiles per state) the contiguous launches also
+    take the XCD-aware tile order (each XCD an eighth of a state's tiles)."""
     rng = np.random.default_rng(4)
-    L = 14
     hs, phis = random_disorder(rng, L, 2)
     spec = pkg.SweepSpec(L=L, T=6, hs=hs, phis=phis, g=0.9, noise_prob=0.1)
     full = engine.autocorr(spec, 6, seed=21, batch=0)
