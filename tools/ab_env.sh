@@ -1,6 +1,7 @@
 #!/bin/bash
-# Development A/B of engine environment switches (not the product): bench.py C2
-# under rocprofv3 --kernel-trace --stats once per setting.
+# Development A/B of engine environment switches (not the product): bench.py (C2,
+# or $BENCH_ARGS, e.g. "--config c4") under rocprofv3 --kernel-trace --stats once
+# per setting.
 # Usage (GPU box, repo root): bash tools/ab_env.sh <tag> "VAR=0" "VAR=1" ...
 set -o pipefail
 TAG=$1; shift
@@ -9,7 +10,7 @@ cd /tmp
 i=0
 for setting in "$@"; do
   i=$((i+1)); n=${TAG}_$i
-  ( export $setting; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_$n -o kt -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/ab_$n.json 2> $O/ab_$n.err ) || { echo "$setting failed"; exit 1; }
+  ( export $setting; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_$n -o kt -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS > $O/ab_$n.json 2> $O/ab_$n.err ) || { echo "$setting failed"; exit 1; }
   python - "$O/ab_$n" "$setting" <<'PY'
 import json, sys, pandas as pd
 d = json.load(open(sys.argv[1] + ".json"))
