@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DTC_ABI_VERSION 11
+#define DTC_ABI_VERSION 12
 
 /* error codes */
 #define DTC_OK 0
@@ -306,7 +306,10 @@ int dtc_energy_device(dtc_ctx* ctx, const dtc_problem* prob, const dtc_device_no
  *   z_sum  [n_inst][T][L], zz_sum [n_inst][T][L-1] (nullable when L = 1),
  *   x_sum  [n_inst][T][L]
  * = the sums over trajectories of dtc_energy's z, zz, x (fixed summation
- * order; equal to the host sums of those rows up to rounding).  The energy
+ * order within a batch, batches added on the host: equal to the host sums of
+ * those rows, and invariant under a change of batch size, only up to
+ * rounding -- unlike the per-trajectory rows, which are bit-identical for any
+ * batching).  The energy
  * scripts need only these means (energy.py:136-173: <H> from the estimator's
  * expectation values); only a few KB per batch cross PCIe. */
 int dtc_energy_sums(dtc_ctx* ctx, const dtc_problem* prob, const dtc_noise* noise,
@@ -336,6 +339,14 @@ int dtc_reset_stats(dtc_ctx* ctx);
  * 12-site window (dtc_lcw3_final, six passes merged; ABI 10).
  * Independent of profiling; lets tests assert which kernel a sweep ran. */
 int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
+/* Batch schedules built since dtc_open (ABI 12; test hook, no reference
+ * counterpart): counts[0] echo chains whose first pass folded into the
+ * forward's dual pass, [1] device-noise batches whose forward ran one kick
+ * layer ahead (one pass per period), [2] device-noise batches rebuilt with K-D
+ * forward passes because a chain did not fold (two passes per period; also set
+ * for every batch under DTC_NO_RUNAHEAD=1, the test switch that forces this
+ * schedule). */
+int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts /* [3] */);
 
 /* Device properties for reports. */
 int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdtc_hip.so")
 KERNEL_KINDS = 6  # DTC_KERNEL_KINDS: lo pass, hi pass, reduce, init, final (measure-only) pass,
                   # virtual-rank exchange
-ABI_VERSION = 11  # DTC_ABI_VERSION of include/dtc.h this binding matches
+ABI_VERSION = 12  # DTC_ABI_VERSION of include/dtc.h this binding matches
 
 # Every symbol declared in include/dtc.h (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "dtc_kernel_stats",
     "dtc_reset_stats",
     "dtc_lightcone_counts",
+    "dtc_schedule_counts",
     "dtc_device_info",
     "dtc_shard_set_basis",
     "dtc_shard_step",
@@ -185,6 +186,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         ]
         lib.dtc_reset_stats.argtypes = [ctypes.c_void_p]
         lib.dtc_lightcone_counts.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
+        lib.dtc_schedule_counts.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
         lib.dtc_device_info.argtypes = [
             ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, P(ctypes.c_int32), _dp,
         ]

@@ -121,6 +121,8 @@ struct dtc_ctx {
   int64_t st_n[DTC_KERNEL_KINDS] = {};
   int64_t lc_launches[4] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
   bool dual = true;  // DTC_NO_DUAL: echo chains start with a pass of their own
+  bool runahead = true;  // DTC_NO_RUNAHEAD: device-noise forward closes periods with K-D
+  int64_t sched_counts[3] = {};  // dtc_schedule_counts: folds, run-ahead, rebuilt
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
   std::vector<Pending> pending;
@@ -1316,6 +1318,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   c->lc_wide = std::getenv("DTC_NO_LCW") == nullptr;
   c->lc_wide3 = c->lc_wide && std::getenv("DTC_NO_LCW3") == nullptr;
   c->dual = std::getenv("DTC_NO_DUAL") == nullptr;
+  c->runahead = std::getenv("DTC_NO_RUNAHEAD") == nullptr;
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1397,6 +1400,12 @@ int dtc_reset_stats(dtc_ctx* ctx) {
 int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts) {
   if (!ctx || !counts) return fail(DTC_EINVAL, "null ctx / counts");
   for (int k = 0; k < 4; ++k) counts[k] = ctx->lc_launches[k];
+  return DTC_OK;
+}
+
+int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts) {
+  if (!ctx || !counts) return fail(DTC_EINVAL, "null ctx / counts");
+  for (int k = 0; k < 3; ++k) counts[k] = ctx->sched_counts[k];
   return DTC_OK;
 }
 
@@ -1639,7 +1648,8 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     // never undone; if any chain does not fold, the schedule is rebuilt with
     // K-D forward passes (two passes per period, nothing run ahead).
     std::vector<Launch> sched;
-    for (bool dev_ahead = rc.device && ctx->dual;;) {
+    bool dev_ahead = rc.device && ctx->dual && ctx->runahead;
+    for (;;) {
     sched.clear();
     bool all_folded = true;
     const bool dev_kd = rc.device && !dev_ahead;  // device-like noise, K-D forward
@@ -1770,7 +1780,12 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     }
     if (!dev_ahead || all_folded) break;
     dev_ahead = false;
+    if (ctx->verbose)
+      std::fprintf(stderr, "[dtc] device-noise schedule rebuilt with K-D forward passes "
+                           "(an echo chain did not fold into the dual pass)\n");
     }
+    for (const Launch& l : sched) ctx->sched_counts[0] += l.dst2 != nullptr;
+    if (rc.device) ++ctx->sched_counts[dev_ahead ? 1 : 2];
     if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipMemcpyAsync(hv_f, ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),

@@ -849,6 +849,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // x_combine adds them after the stores, off the tile's chain)
   auto x_now = [&](auto lay_tag, double scale, int slot0) {
     constexpr int LAY = decltype(lay_tag)::value;
+    // s_xpart has a slot per wave only in the three-per-CU energy pass: any
+    // other instantiation reaching here would write past it
+    static_assert(SPLIT && MC == 3, "x_now: s_xpart sized for SPLIT && MC == 3 only");
     double a[4];
     pair_sums(lay_tag, a, scale);
     double u0 = a[0], w0 = a[2], u1 = a[1], w1 = a[3];
@@ -864,12 +867,14 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   };
   auto measure_x_post = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
-    if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPost);
+    if constexpr (MC != 3) return;
+    else if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPost);
     else pair_sums(lay_tag, xpost[LAY], scale);
   };
   auto measure_x_pre = [&](auto lay_tag, double scale) {
     constexpr int LAY = decltype(lay_tag)::value;
-    if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPre);
+    if constexpr (MC != 3) return;
+    else if constexpr (SPLIT) x_now(lay_tag, scale, kSlotXPre);
     else pair_sums(lay_tag, xpre[LAY], scale);
   };
   // squared share of the global factor carried by the factored kicks of
@@ -1138,7 +1143,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       const int tb = site < c ? site : ((site >= s && site < s + kTileBits - c) ? c + site - s : -1);
       double acc = 0.0;
       if (tb >= 0 && ((A.act >> tb) & 1) && (pre ? x_pre : x_post)) {
-        if constexpr (SPLIT) {
+        if constexpr (SPLIT && MC == 3) {
           const double* px = &s_xpart[0][pre ? 1 : 0][tb >> 2][(tb & 3) << 3];
           constexpr int kW = 2 * 3 * 32;  // doubles per wave
           for (int w = 0; w < kThreads / 64; ++w)

@@ -421,6 +421,15 @@ class DtcEngine:
         _capi.check(self._lib.dtc_lightcone_counts(self._ctx, c))
         return {"lc8": c[0], "lcw": c[1], "lcw2": c[2], "lcw3": c[3]}
 
+    def schedule_counts(self):
+        """Batch schedules built since the engine opened (dtc_schedule_counts):
+        echo chains folded into a dual pass, device-noise batches whose forward
+        ran a layer ahead, and device-noise batches run with K-D forward passes
+        (a chain did not fold, or DTC_NO_RUNAHEAD=1)."""
+        c = (ctypes.c_int64 * 3)()
+        _capi.check(self._lib.dtc_schedule_counts(self._ctx, c))
+        return {"folded": c[0], "device_runahead": c[1], "device_kd": c[2]}
+
     def device_info(self):
         name = ctypes.create_string_buffer(256)
         ncu = ctypes.c_int32()

@@ -41,13 +41,14 @@ def test_library_is_gfx950_code_object(pkg):
 
 def test_abi_version_and_null_errors(pkg):
     lib = pkg._capi.load_library()
-    assert lib.dtc_abi_version() == 11 == pkg._capi.ABI_VERSION
+    assert lib.dtc_abi_version() == 12 == pkg._capi.ABI_VERSION
     # null context / arguments are rejected before any device call
     assert lib.dtc_autocorr(None, None, None, 0, 0, 1, None, None, None) == -1
     assert b"null" in lib.dtc_last_error()
     assert lib.dtc_close(None) == 0
     assert lib.dtc_set_profiling(None, 1) == -1
     assert lib.dtc_lightcone_counts(None, None) == -1
+    assert lib.dtc_schedule_counts(None, None) == -1
     assert lib.dtc_shard_kick_exchange_slice(None, None, None, None, 0, 0, 1, 0, 0, 0, None) == -1
 
 

@@ -265,16 +265,65 @@ def test_device_dual_pass(pkg, monkeypatch, L, T, state, pol, toff):
                 eng.set_profiling(True)
                 out = eng.autocorr(spec, 3, seed=29)
                 st = eng.kernel_stats()
-        return out, st[pkg._capi.KERNEL_LO_PASS]["launches"] + st[pkg._capi.KERNEL_HI_PASS]["launches"]
+                cnt = eng.schedule_counts()
+        return (out, st[pkg._capi.KERNEL_LO_PASS]["launches"]
+                + st[pkg._capi.KERNEL_HI_PASS]["launches"], cnt)
 
-    got, n_dual = run(False)
-    ref, n_single = run(True)
+    got, n_dual, cnt = run(False)
+    ref, n_single, cnt_ref = run(True)
     want = c_oracle.autocorr(spec, 3, seed=29)
     for k in want:
         assert float(np.abs(got[k] - want[k]).max()) < 1e-10, k
     assert np.abs(got["echo"] - ref["echo"]).max() < 1e-12
     assert np.abs(got["fwd"] - ref["fwd"]).max() < 1e-13
     assert n_dual < n_single
+    # the run-ahead schedule was kept (no silent rebuild with K-D forward
+    # passes, which would double the forward passes per period) -- except for
+    # one site group (L <= 12): its t = 1 chain is a single pass (undo D^* K'_1),
+    # nothing to fold it into, and the undo of a Kraus kick cannot run, so such
+    # plans take the K-D schedule, its chains folded into dtc_kd_dual
+    if L > 12:
+        assert cnt["device_kd"] == 0 and cnt["device_runahead"] == 1 and cnt["folded"] > 0, cnt
+    else:
+        assert cnt["device_kd"] == 1 and cnt["device_runahead"] == 0 and cnt["folded"] > 0, cnt
+    assert cnt_ref == {"folded": 0, "device_runahead": 0, "device_kd": 1}, cnt_ref
+
+
+@pytest.mark.parametrize("L,T,pol", [(14, 6, "x"), (20, 5, "circular_left")])
+def test_device_kd_dual_forced(pkg, monkeypatch, L, T, pol):
+    """The K-D schedule under device-like noise, forced (DTC_NO_RUNAHEAD=1: the
+    schedule the engine falls back to when an echo chain cannot fold into the
+    run-ahead dual pass): the forward closes each period with a K-D pass and
+    every chain's first D^* K'_1 pass folds into it (dtc_kd_dual).  Per
+    trajectory: the oracle's values (1e-10) and the run-ahead schedule's
+    (1e-12), with more forward passes than the run-ahead schedule."""
+    rng = np.random.default_rng(L * 5 + T)
+    hs, phis = random_disorder(rng, L, 1)
+    spec = pkg.SweepSpec(L=L, T=T, hs=hs, phis=phis, g=0.93, polarization=pol,
+                         initial_state="neel", device=harsh_device(pkg, L))
+
+    def run(forced):
+        with monkeypatch.context() as m:
+            if forced:
+                m.setenv("DTC_NO_RUNAHEAD", "1")
+            with pkg.DtcEngine(0) as eng:
+                eng.set_profiling(True)
+                out = eng.autocorr(spec, 4, seed=31)
+                st = eng.kernel_stats()
+                cnt = eng.schedule_counts()
+        return (out, st[pkg._capi.KERNEL_LO_PASS]["launches"]
+                + st[pkg._capi.KERNEL_HI_PASS]["launches"], cnt)
+
+    kd, n_kd, cnt_kd = run(True)
+    ahead, n_ahead, cnt_ahead = run(False)
+    want = c_oracle.autocorr(spec, 4, seed=31)
+    for k in want:
+        assert float(np.abs(kd[k] - want[k]).max()) < 1e-10, k
+        assert float(np.abs(kd[k] - ahead[k]).max()) < 1e-12, k
+    assert cnt_kd["device_kd"] == 1 and cnt_kd["device_runahead"] == 0, cnt_kd
+    assert cnt_kd["folded"] > 0, cnt_kd  # the K-D dual pass ran
+    assert cnt_ahead["device_kd"] == 0, cnt_ahead
+    assert n_kd > n_ahead
 
 
 def test_device_dual_batches_and_t_first(pkg, engine):

@@ -164,3 +164,21 @@ def test_energy_sums_match_trajectory_rows(pkg, engine, L, T, n_inst, n_traj, ba
                                                          0.93, hs[i], phis[i], "full")
                       for i in range(n_inst)])
     assert np.abs(e - ref_e).max() < 1e-11
+    # the previous estimator, pinned independently of the affinity the sums
+    # rely on: <H> (and the read-out map) per trajectory row, then the mean
+    # over trajectories
+    readout = None
+    if device:
+        readout = (np.linspace(0.01, 0.04, L), np.linspace(0.03, 0.005, L))
+    per_traj = []
+    for i in range(n_inst):
+        row = []
+        for r in range(n_traj):
+            o = {k: v[i, r] for k, v in rows.items()}
+            if readout is not None:
+                o = pkg.energy.readout_observables(o, *readout)
+            row.append(pkg.energy.energy_from_observables(o, L, 0.93, hs[i], phis[i], "full"))
+        per_traj.append(np.mean(row, axis=0))
+    e_ro = pkg.energy.get_instances_energy(spec, n_traj, seed=44, engine=engine, traj_offset=3,
+                                           readout=readout)["full"]
+    assert np.abs(e_ro - np.stack(per_traj)).max() < 1e-11

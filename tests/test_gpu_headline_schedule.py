@@ -134,8 +134,10 @@ def test_c3_schedule_long_chains_match_oracle(pkg, engine):
     ids 7, 1023 and 1024 equal the gate-by-gate device oracle at 1e-10 on the
     longest echo chains (t = 26..29, the oracle run with t_first = 26 to bound
     its cost; the engine's values at t >= t_first do not depend on t_first),
-    fwd and echo.  Exercises the device dual pass (dtc_kd_dual) and the
-    kick-only ends at the line's own batch."""
+    fwd and echo.  Exercises the run-ahead forward with the device K-D-K dual
+    pass (dtc_kdk_dual; the K-D form dtc_kd_dual is the fallback schedule,
+    test_gpu_device.py::test_device_kd_dual_forced) and the kick-only ends at
+    the line's own batch: the run-ahead schedule must be the one that ran."""
     _free_device_memory(engine)
     spec = _spec(pkg)
     cal = pkg.DeviceCalibration.from_json(os.path.join(ROOT, "data", "device_standin_L20.json"))
@@ -150,6 +152,7 @@ def test_c3_schedule_long_chains_match_oracle(pkg, engine):
 
     with ThreadPoolExecutor(len(ids)) as ex:
         ref = dict(zip(ids, ex.map(one, ids)))
+    before = engine.schedule_counts()
     for off in (0, B):
         got = engine.autocorr(spec, B, seed=SEED, traj_offset=off, batch=B)
         for g in ids:
@@ -158,4 +161,7 @@ def test_c3_schedule_long_chains_match_oracle(pkg, engine):
             for k, r in zip(("fwd", "echo"), ref[g]):
                 err = float(np.abs(got[k][0, g - off, 26:] - r[26:]).max())
                 assert err < TOL, (k, g, err)
+    after = engine.schedule_counts()
+    assert after["device_runahead"] - before["device_runahead"] == 2, (before, after)
+    assert after["device_kd"] == before["device_kd"], (before, after)
     engine.release_buffers()

@@ -152,10 +152,14 @@ __device__ __forceinline__ void kdk_probe(double2* __restrict__ st, int og, int 
     diag();
     kicks(K1{}); swap16();
     kicks(K4{}); xch(P_(8), P_(0)); kicks(K4{}); xch(P_(0), P_(4)); kicks(K4{});
-  } else {  // B13: IO 9 (sites 16..19) -> 5 (col 5, sites 13..15) | D | back
+  } else if constexpr (PROG == 3) {  // B13: IO 9 (sites 16..19) -> 5 (col 5, sites 13..15) | D | back
     kicks(K4{}); xch(P_(9), P_(5)); kicks(K3{});
     diag();
     kicks(K3{}); xch(P_(5), P_(9)); kicks(K4{});
+  } else {  // B13c5 (round 6): 8 sites 12..19 over 512-B columns: IO 9 (sites 16..19) -> 5 (12..15) | D | back
+    kicks(K4{}); xch(P_(9), P_(5)); kicks(K4{});
+    diag();
+    kicks(K4{}); xch(P_(5), P_(9)); kicks(K4{});
   }
 #undef P_
 #pragma unroll
@@ -221,6 +225,11 @@ int main(int argc, char** argv) {
     RUN("A13 c=13, half-tile LDS, 2 WG/CU", 13, 13, true, 4, 2, 2);
     RUN("B13 c=6 s=13, full-tile LDS, 1 WG/CU", 13, 6, false, 9, 3, 1);
     RUN("B13 c=6 s=13, half-tile LDS, 2 WG/CU", 13, 6, true, 9, 3, 2);
+    // round 6: the 12/8 split kept, only the 8-site column pass on a 13-bit
+    // tile (5 column bits: 512-B runs, half an octet run)
+    RUN("B13c5 c=5 s=12 (8 sites), half-tile LDS, 2 WG/CU", 13, 5, true, 9, 4, 2);
+    RUN("B13c5 c=5 s=12 (8 sites), full-tile LDS, 1 WG/CU", 13, 5, false, 9, 4, 1);
+    RUN("B12 c=4 s=12, half-tile LDS, 3 WG/CU", 12, 4, true, 8, 1, 3);
   }
   return 0;
 }
