@@ -28,7 +28,7 @@ OBJDIR  := build/obj
 LIB     := $(PKG)/lib/libdtc_hip.so
 ORACLE  := oracle/liboracle.so
 ORACLE3 := oracle/liboracle_v3.so
-SRCS    := $(PKG)/csrc/dtc_kernels.hip $(PKG)/csrc/dtc_lightcone.hip $(PKG)/csrc/dtc_engine.cpp
+SRCS    := $(PKG)/csrc/dtc_kernels.hip $(PKG)/csrc/dtc_lightcone.hip $(PKG)/csrc/dtc_tile13.hip $(PKG)/csrc/dtc_engine.cpp
 HDRS    := $(PKG)/csrc/dtc_kernels.h $(PKG)/csrc/dtc_device.h $(PKG)/csrc/dtc_rng.h include/dtc.h
 
 all: $(LIB) $(ORACLE) $(ORACLE3)
@@ -45,11 +45,16 @@ $(OBJDIR)/dtc_lightcone.o: $(PKG)/csrc/dtc_lightcone.hip $(HDRS)
 	@rm -f $@
 	$(HIPCC) $(HIPCFLAGS) $(KFLAGS) -c $< -o $@ 2> $@.log; rc=$$?; grep -v "not a recognized feature" $@.log >&2; exit $$rc
 
+$(OBJDIR)/dtc_tile13.o: $(PKG)/csrc/dtc_tile13.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	@rm -f $@
+	$(HIPCC) $(HIPCFLAGS) $(KFLAGS) -c $< -o $@ 2> $@.log; rc=$$?; grep -v "not a recognized feature" $@.log >&2; exit $$rc
+
 $(OBJDIR)/dtc_engine.o: $(PKG)/csrc/dtc_engine.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPCFLAGS) -c $< -o $@
 
-$(LIB): $(OBJDIR)/dtc_kernels.o $(OBJDIR)/dtc_lightcone.o $(OBJDIR)/dtc_engine.o
+$(LIB): $(OBJDIR)/dtc_kernels.o $(OBJDIR)/dtc_lightcone.o $(OBJDIR)/dtc_tile13.o $(OBJDIR)/dtc_engine.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared $^ -o $@
 

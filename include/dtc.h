@@ -342,11 +342,12 @@ int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
 /* Batch schedules built since dtc_open (ABI 12; test hook, no reference
  * counterpart): counts[0] echo chains whose first pass folded into the
  * forward's dual pass, [1] device-noise batches whose forward ran one kick
- * layer ahead (one pass per period), [2] device-noise batches rebuilt with K-D
- * forward passes because a chain did not fold (two passes per period; also set
- * for every batch under DTC_NO_RUNAHEAD=1, the test switch that forces this
- * schedule). */
-int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts /* [3] */);
+ * layer ahead (one pass per period), [2] device-noise batches run with K-D
+ * forward passes (a chain did not fold, or DTC_NO_RUNAHEAD=1, the test switch
+ * that forces this schedule; two passes per period), [3] batches run with the
+ * 13 / 7 site split of L = 20 (a 13-site group in 8192-amplitude tiles, a
+ * 7-site column group; DTC_NO_SPLIT13=1 keeps the 12 / 8 split). */
+int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
 
 /* Device properties for reports. */
 int dtc_device_info(dtc_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,

@@ -136,13 +136,15 @@ struct RecScalar {
   __device__ __forceinline__ int i(int rec, int e) const { return (int)p[8 * rec + e]; }
 };
 
-template <int N, int KIND, typename Rec>
+template <int N, int KIND, int QM = 15, typename Rec>
 __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, int rec0) {
   // Every site of an active nibble runs (inactive sites carry the identity):
   // no data-dependent branches, so no register shuffles at merge points; the
-  // RX/RY variant branch is wave-uniform.
+  // RX/RY variant branch is wave-uniform.  QM: the register bits that hold
+  // sites at all (the 7-site column group's nibble 1 starts with a column bit)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
+    if (!((QM >> q) & 1)) continue;
     const int k = rec0 + 4 * N + q;
     if (KIND == kKindGen) {
       double2 m[4];
@@ -369,6 +371,19 @@ __device__ __forceinline__ void swap_rows(double& a, double& b) {
     const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
     a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
     b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
+  }
+}
+
+// register bit Q <-> lane bit 4 (M = 16) or 5 (M = 32), for the whole tile
+// (32 permlane swaps, no LDS, no barrier): the light-cone ends' row swaps and
+// the 13-site pass's fifth register site (dtc_tile13.hip)
+template <int Q, int M>
+__device__ __forceinline__ void swap_reg_lane(double2 (&v)[kRegs]) {
+#pragma unroll
+  for (int r = 0; r < kRegs; ++r) {
+    if (r & (1 << Q)) continue;
+    swap_rows<M>(v[r].x, v[r | (1 << Q)].x);
+    swap_rows<M>(v[r].y, v[r | (1 << Q)].y);
   }
 }
 

@@ -68,8 +68,9 @@ struct HostBuf {
 
 
 struct Group {
-  int c, s;  // tile = bits [0, c) + [s, s + 12 - c)
+  int c, s;  // tile = bits [0, c) + [s, s + tb - c)
   int act;   // active tile-bit mask
+  int tb = dtc::kTileBits;  // tile bits: 12, or 13 (the 13-site group, dtc_tile13.hip)
 };
 
 struct Pending {
@@ -122,7 +123,8 @@ struct dtc_ctx {
   int64_t lc_launches[4] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
   bool dual = true;  // DTC_NO_DUAL: echo chains start with a pass of their own
   bool runahead = true;  // DTC_NO_RUNAHEAD: device-noise forward closes periods with K-D
-  int64_t sched_counts[3] = {};  // dtc_schedule_counts: folds, run-ahead, rebuilt
+  bool split13 = true;   // DTC_NO_SPLIT13: L = 20 sweeps keep the 12 / 8 site groups
+  int64_t sched_counts[4] = {};  // dtc_schedule_counts: folds, run-ahead, rebuilt, 13 / 7
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
   std::vector<Pending> pending;
@@ -224,7 +226,13 @@ struct Plan {
 // group holding the top bits (the bits an exchange swaps with the rank bits)
 // is a large one and the pre-exchange kicks stay below a few free bits of it
 // (the slices of dtc_shard_kick_slice).
-Plan make_plan(int L, bool largest_top = false) {
+// split13 (round 6, L = 20 only): a 13-site group at tile bits 0..12
+// (dtc_tile13.hip) and a 7-site column group, tile bits 0..4 + sites 13..19
+// (pass_body kGeoB7) -- the column pass kicks 7 sites over 512-B runs instead
+// of 8 over 256-B runs (tools/tile13_kdk_probe.hip, profiles/r6c_*).
+// pl.n_tiles is then the larger group's tile count (buffer sizes); a pass's
+// own is 2^(L_eff - tb).
+Plan make_plan(int L, bool largest_top = false, bool split13 = false) {
   Plan pl;
   pl.L = L;
   pl.L_eff = std::max(L, dtc::kTileBits);
@@ -232,6 +240,12 @@ Plan make_plan(int L, bool largest_top = false) {
   pl.n_tiles = 1 << (pl.L_eff - dtc::kTileBits);
   pl.n_chunks = (pl.L_eff + dtc::kChunkBits - 1) / dtc::kChunkBits;
   pl.diag_stride = (pl.n_chunks + pl.L_eff) * 64;
+  if (split13 && L == 20) {
+    pl.groups.push_back(Group{dtc::kMaxTileBits, dtc::kMaxTileBits, (1 << dtc::kMaxTileBits) - 1,
+                              dtc::kMaxTileBits});
+    pl.groups.push_back(Group{dtc::kB7Cols, dtc::kMaxTileBits, 0xFE0, dtc::kTileBits});
+    return pl;
+  }
   if (L <= dtc::kTileBits) {
     // one group; the padding sites L..11 get identity kicks (kernel) so the
     // whole 12-bit tile runs the standard round plan
@@ -548,6 +562,7 @@ dtc::PassKick pass_kick(const RunCfg& rc, const PassSpec& ps) {
   pk.c = g.c;
   pk.s = g.s;
   pk.act = g.act;
+  pk.tb = g.tb;
   return pk;
 }
 
@@ -611,7 +626,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
       }
     }
   }
-  if (ps.diag != dtc::kDiagNone) {
+  if (ps.diag != dtc::kDiagNone && g.tb == dtc::kTileBits && g.c != dtc::kB7Cols) {
     // the kernel's diagonal uses the window table of the register nibble it
     // is applied in (RoundPlan::d_lay): that nibble must not straddle c
     // (same rule as RoundPlan: load/store layout IO, other high nibble O)
@@ -632,6 +647,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.c = g.c;
   A.s = g.s;
   A.tile_bits_mid = g.s - g.c;
+  A.tile_bits = g.tb;
   A.act = g.act;
   A.recs = recs;
   A.diag_conj = ps.diag == dtc::kDiagConj;
@@ -677,7 +693,7 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
     ctx->pending.push_back(Pending{kernel, e0, e1, per_amp * (double)((int64_t)1 << A.L_eff) * batch});
   }
   if (meas_mode != dtc::kMeasNone && meas_out)
-    DTC_TRY(launch_reduce_prof(ctx, rc.pl.n_tiles, n_obs, batch, meas_out, meas_stride));
+    DTC_TRY(launch_reduce_prof(ctx, 1 << (A.L_eff - g.tb), n_obs, batch, meas_out, meas_stride));
   return DTC_OK;
 }
 
@@ -1061,7 +1077,7 @@ void shard_chain(const dtc_problem* pr, const dtc_shard* sh, int inst, int rank,
 
 uint64_t group_bits(const Group& g) {
   uint64_t m = 0;
-  for (int k = 0; k < dtc::kTileBits; ++k)
+  for (int k = 0; k < g.tb; ++k)
     if (g.act & (1 << k)) m |= 1ull << (k < g.c ? k : g.s + k - g.c);
   return m;
 }
@@ -1070,7 +1086,7 @@ uint64_t group_bits(const Group& g) {
 // k.skip), below L.
 uint64_t layer_sites(const Group& g, const KickDesc& k, int L) {
   uint64_t m = 0;
-  for (int b = 0; b < dtc::kTileBits; ++b) {
+  for (int b = 0; b < g.tb; ++b) {
     if (!(g.act & ~(int)k.skip & (1 << b))) continue;
     const int site = b < g.c ? b : g.s + b - g.c;
     if (site < L) m |= 1ull << site;
@@ -1081,7 +1097,7 @@ uint64_t layer_sites(const Group& g, const KickDesc& k, int L) {
 // tile bits of group g that are NOT in mask (left identity by a kick layer)
 uint32_t skip_bits(const Group& g, uint64_t mask) {
   uint32_t sk = 0;
-  for (int k = 0; k < dtc::kTileBits; ++k) {
+  for (int k = 0; k < g.tb; ++k) {
     if (!(g.act & (1 << k))) continue;
     const int bit = k < g.c ? k : g.s + k - g.c;
     if (!((mask >> bit) & 1)) sk |= 1u << k;
@@ -1319,6 +1335,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   c->lc_wide3 = c->lc_wide && std::getenv("DTC_NO_LCW3") == nullptr;
   c->dual = std::getenv("DTC_NO_DUAL") == nullptr;
   c->runahead = std::getenv("DTC_NO_RUNAHEAD") == nullptr;
+  c->split13 = std::getenv("DTC_NO_SPLIT13") == nullptr;
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1405,7 +1422,7 @@ int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts) {
 
 int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts) {
   if (!ctx || !counts) return fail(DTC_EINVAL, "null ctx / counts");
-  for (int k = 0; k < 3; ++k) counts[k] = ctx->sched_counts[k];
+  for (int k = 0; k < 4; ++k) counts[k] = ctx->sched_counts[k];
   return DTC_OK;
 }
 
@@ -1528,12 +1545,18 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
 
   RunCfg rc;
   rc.prob = pr;
-  rc.pl = make_plan(pr->L);
   rc.seed = seed;
   rc.traj_offset = traj_offset;
   rc.n_traj = n_traj;
   rc.noisy = nz->p > 0.0 ? 1 : 0;
   rc.row_kind = classify_rows(pr);
+  {
+    // the 13 / 7 split where its kernels cover every pass: L = 20, unitary
+    // factored kicks (RX / RY rows), the probe measurement only, no prefix
+    bool s13 = ctx->split13 && pr->L == 20 && !dv && !zsite && !use_prefix;
+    for (int k : rc.row_kind) s13 = s13 && (k == dtc::kKindRX || k == dtc::kKindRY);
+    rc.pl = make_plan(pr->L, false, s13);
+  }
   thresholds(nz->p, &rc.thr1, &rc.thr2, &rc.thr3);
   if (dv) DTC_TRY(setup_device_noise(ctx, pr, dv, rc));
   const Plan& pl = rc.pl;
@@ -1738,6 +1761,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
           const int es = dev_kd ? dtc::kShapeDK : dtc::kShapeKDK;
           // (the dual kernels carry the probe at most: not with per-site Z)
           const bool fok = pass_shape(f.ps) == fs && !f.basis && f.src == F &&
+                           pl.groups[f.ps.group].tb == dtc::kTileBits &&
                            (f.meas_mode == dtc::kMeasNone || f.meas_mode == dtc::kMeasProbe);
           const bool eok =
               pass_shape(e.ps) == es && e.ps.lc_w0 < 0 && e.ps.group == f.ps.group &&
@@ -1786,6 +1810,7 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     }
     for (const Launch& l : sched) ctx->sched_counts[0] += l.dst2 != nullptr;
     if (rc.device) ++ctx->sched_counts[dev_ahead ? 1 : 2];
+    if (pl.groups[0].tb == dtc::kMaxTileBits) ++ctx->sched_counts[3];
     if (!use_prefix) DTC_TRY(basis_source(ctx, sched, F, pl.len, nb, octet));
     DTC_TRY(run_launches(ctx, rc, bs, nb, sched));
     DTC_HIP(hipMemcpyAsync(hv_f, ctx->vals_f.p, (size_t)nb * T * n_obs_f * sizeof(double),

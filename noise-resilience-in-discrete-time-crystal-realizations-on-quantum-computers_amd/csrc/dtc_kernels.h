@@ -34,6 +34,11 @@ static constexpr int kRedSlots = kSlotXPost + kTileBits;
 constexpr int io_layout(int nibs) { return ((DTC_IO1_NIBS >> nibs) & 1) ? 1 : 2; }
 
 enum DiagMode { kDiagNone = 0, kDiagFwd = 1, kDiagConj = 2 };
+// Tile geometries of the 12-bit passes (pass_body GEO): the plan's standard
+// groups, and the 7-site column group of the 13 / 7 split (c = 5, s = 13:
+// tile bits 0..4 = global 0..4, 5..11 = sites 13..19; act 0xFE0).
+enum TileGeo { kGeoStd = 0, kGeoB7 = 1 };
+static constexpr int kB7Cols = 5;
 enum MeasMode {
   kMeasNone = 0,
   kMeasProbe = 1,   // (norm, Z_probe)
@@ -167,7 +172,10 @@ union KickRec {
   double d[8];
   long long i[8];
 };
-static constexpr int kRecPerState = 2 * kTileBits + 1;
+// (blocks of 27 records: room for the 13-bit tile of dtc_tile13.hip, whose
+// records are pre k, post 13 + k, total 26; the 12-bit passes use 0..24)
+static constexpr int kMaxTileBits = 13;
+static constexpr int kRecPerState = 2 * kMaxTileBits + 1;
 static constexpr int kRecTotal = 2 * kTileBits;
 
 // One pass's kick layers, as the prep kernel needs them.
@@ -175,6 +183,7 @@ struct PassKick {
   KickDesc pre, post;   // enabled = 0: no such layer
   int kind;             // KickKind of the pass
   int c, s, act;        // tile geometry (see PassArgs)
+  int tb;               // tile bits (12; 13: dtc_tile13.hip's records 13 + k, 26)
   int lc_layers;        // kShapeLC: layers lc[0 .. lc_layers), site b of layer l kicked
   KickDesc lc[kLcMaxLayers];  // when bit 8 l + b of lc_mask is set (window site b = tile
   uint64_t lc_mask;     // bit 4 + b); Pauli-frame records (kLcCoefs ..)
@@ -223,6 +232,8 @@ struct PassArgs {
   int L_real;              // physical sites
   int c, s;                // tile geometry
   int tile_bits_mid;       // s - c  (tile-id bits deposited at [c, s))
+  int tile_bits;           // 12 (dtc_kernels.hip), 13 (dtc_tile13.hip: c = 13, the
+                           // low 13-site group of the 13 / 7 split)
   int act;                 // active tile-bit mask (sites kicked by this pass)
   // batch -> instance: inst = (batch_start + b) / n_traj
   int batch;               // states in this launch
@@ -295,6 +306,11 @@ hipError_t launch_prep(const PrepArgs& a, hipStream_t stream);
 // (kLcVariant* below)
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream,
                        int* lc_variant = nullptr);
+
+// Passes over a 13-site group at tile bits 0..12 (dtc_tile13.hip; tile_bits 13,
+// c = 13): K-D-K, K-D, D-K, K, D shapes, factored RX / RY kicks, the probe
+// measurement at most, no dual pass, no basis source.
+hipError_t launch_pass13(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream);
 
 // kShapeLC passes (dtc_lightcone.hip), from launch_pass with its grid
 enum LcVariant { kLcVariant8 = 0, kLcVariantWide = 1, kLcVariantWide2 = 2, kLcVariantWide3 = 3 };

@@ -360,9 +360,10 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   }
   int ksum = 0;
   double w[2] = {1.0, 1.0};
+  const int tb = pk.tb == kMaxTileBits ? kMaxTileBits : kTileBits;
   for (int half = 0; half < 2; ++half) {
     const KickDesc& K = half == 0 ? pk.pre : pk.post;
-    for (int k = 0; k < kTileBits; ++k) {
+    for (int k = 0; k < tb; ++k) {
       const int lsite = k < pk.c ? k : pk.s + k - pk.c;
       double2 m[4] = {make_double2(1.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0),
                       make_double2(1.0, 0.0)};
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
         r.d[2] = sm.scale * sm.scale;
         for (int e = 3; e < 8; ++e) r.d[e] = 0.0;
       }
-      out[half * kTileBits + k] = r;
+      out[half * tb + k] = r;
       ksum += sm.k;
       w[half] *= sm.scale;
     }
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   tot.d[0] = kph == 0 ? wg : (kph == 2 ? -wg : 0.0);
   tot.d[1] = kph == 1 ? wg : (kph == 3 ? -wg : 0.0);
   tot.d[2] = 1.0 / (w[1] * w[1]);
-  out[kRecTotal] = tot;
+  out[2 * tb] = tot;
 }
 
 hipError_t launch_prep(const PrepArgs& a, hipStream_t stream) {
@@ -453,10 +454,21 @@ struct RoundPlan {
 // the pre-kick the tile is copied; the copy takes the echo chain's first kick
 // layer (A.recs2's post-kick, its global factor A.recs2's total) and is stored
 // to A.dst2, then the pass goes on (diagonal, probe, post-kick, store to dst).
+// GEO: tile geometry.  kGeoStd: the plan's groups (column bits at a nibble
+// boundary, the diagonal's register nibble inside or outside them).  kGeoB7
+// (round 6, the 13 / 7 split of L = 20, dtc_tile13.hip): the 7-site column
+// group, tile bits 0..4 = global 0..4 (512-B runs), 5..11 = sites 13..19 --
+// register nibble 1 holds column bit 4 (no kick: QM 14) and sites 13..15, so
+// its diagonal is two window tables (start bits 4 and 13), see diag_in.
 template <int SHAPE, int NIBS, int KIND, int MC = 0, bool NS = false, bool SPLIT = false,
-          bool DUAL = false>
+          bool DUAL = false, int GEO = kGeoStd>
 __device__ __forceinline__ void pass_body(const PassArgs& A) {
   using RP = RoundPlan<NIBS, SHAPE>;
+  static_assert(GEO == kGeoStd || (NIBS == 6 && (KIND == kKindRX || KIND == kKindRY) && MC <= 1),
+                "the 7-site column geometry: factored unitary kicks, the probe at most");
+  // register bits of nibble N that hold sites
+  constexpr auto qm = [](int N) { return (GEO == kGeoB7 && N == 1) ? 14 : 15; };
+  constexpr bool kSplitDiag = GEO == kGeoB7 && RP::d_lay == 1;
   static_assert(!DUAL || (MC <= 1 && !NS &&
                           ((SHAPE == kShapeKDK &&
                             (KIND == kKindRX || KIND == kKindRY || KIND == kKindGen ||
@@ -476,6 +488,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   __shared__ double s_half2[(DUAL && SHAPE == kShapeKDK) ? kHalfSlots : 1];
   __shared__ double2 s_chunk[RP::diag ? kMaxChunks * 64 : 1];
   __shared__ double2 s_win[RP::diag ? 64 : 1];
+  __shared__ double2 s_win2[kSplitDiag ? 64 : 1];  // kGeoB7: the window of start bit s
   __shared__ double s_red[kThreads / 64][kRedSlots];
   // three-per-CU energy passes: per wave, X point (post, pre), nibble, the
   // eight lane partials of the nibble's four sites (x_now)
@@ -536,11 +549,13 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // tile's (vector memory returns in order), staged to LDS below ----
   constexpr int kChunkPerThread = (kMaxChunks * 64 + kThreads - 1) / kThreads;
   double2 dchunk[kChunkPerThread];
-  double2 dwin = make_double2(1.0, 0.0);
+  double2 dwin = make_double2(1.0, 0.0), dwin2 = make_double2(1.0, 0.0);
   int g0 = -1;
   if (RP::diag) {
     const int tb = 4 * RP::d_lay;
-    g0 = tb >= c ? s + tb - c : (tb + 4 <= c ? tb : -1);
+    // (kGeoB7, nibble 1: the window of start bit 4 = the column bit c - 1, and
+    // of start bit s below)
+    g0 = kSplitDiag ? c - 1 : (tb >= c ? s + tb - c : (tb + 4 <= c ? tb : -1));
     const double2* dt = A.diag + (int64_t)inst * A.diag_stride;
 #pragma unroll
     for (int j = 0; j < kChunkPerThread; ++j) {
@@ -548,6 +563,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       if (i < A.n_chunks * 64) dchunk[j] = dt[i];
     }
     if (g0 >= 0 && t < 64) dwin = dt[(A.n_chunks + g0) * 64 + t];
+    if (kSplitDiag && t < 64) dwin2 = dt[(A.n_chunks + s) * 64 + t];
   }
 
   // ---- the tile (coalesced 16-B loads: uniform 64-bit base + one per-lane
@@ -617,6 +633,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
     }
     if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    if (kSplitDiag && t < 64) s_win2[t] = make_double2(dwin2.x, cs * dwin2.y);
     // made visible by the first exchange's barrier, or by this one
     if constexpr (!(RP::pre && (RP::n0 || RP::nO))) __syncthreads();
   }
@@ -631,6 +648,22 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   auto diag_in = [&](auto lay_tag, bool with_g) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int64_t x0 = M.at(ybase<LAY>(t));
+    if constexpr (kSplitDiag && LAY == 1) {
+      // kGeoB7: register bit 0 = global bit c - 1 = 4, bits 1..3 = s .. s + 2:
+      // no term of D couples them, so D(x) = D(x0) Wa(x) / Wa(x0) Wb(x) / Wb(x0)
+      // with Wa, Wb the windows of start bits 4 and s (bits [3, 9), [s - 1,
+      // s + 5)); the thread's two values of D(x0) / Wa(x0) / Wb(x0) Wa(x) are
+      // formed once, then one lookup and two complex products per amplitude
+      const int ia = (int)(((x0 << 1) >> (c - 1)) & 63), ib = (int)(((x0 << 1) >> s) & 63);
+      const double2 wa = s_win[ia], wb = s_win2[ib];
+      const double2 pc = cmul(cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(wa.x, -wa.y)),
+                                   make_double2(wb.x, -wb.y)),
+                              with_g ? gph : make_double2(1.0, 0.0));
+      const double2 q[2] = {cmul(pc, wa), cmul(pc, s_win[ia | 2])};
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(q[r & 1], s_win2[ib | ((r >> 1) << 1)]));
+      return;
+    }
     // D(x) = P_C * W[x], P_C = D(x0) / W[x0] (x the global phase) thread
     // constant, W indexed by bits [g0-1, g0+5) of x: one LDS lookup and two
     // complex products per amplitude (the engine's site groups keep the
@@ -932,19 +965,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     double sc = 1.0;
     if constexpr (RP::nIO) {
       if (x_pre) measure_x_pre(LIO{}, sc);
-      apply_nibble<RP::IO, KIND>(v, R, 0);
+      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, 0);
       if (x_pre) sc *= nib_w2(RP::IO, 0);
     }
     if constexpr (RP::n0) {
       xch_tile<SPLIT, RP::IO, 0>(v, s_tile, s_half, t);
       if (x_pre) measure_x_pre(L0{}, sc);
-      apply_nibble<0, KIND>(v, R, 0);
+      apply_nibble<0, KIND, qm(0)>(v, R, 0);
       if (x_pre) sc *= nib_w2(0, 0);
     }
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, s_half, t);
       if (x_pre) measure_x_pre(LO{}, sc);
-      apply_nibble<RP::O, KIND>(v, R, 0);
+      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, 0);
     }
   }
   DTC_TS(3);
@@ -973,15 +1006,15 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::d_lay, RP::O>(w, s_tile, s_half, t);
-      apply_nibble<RP::O, KIND>(w, R2, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O)>(w, R2, kTileBits);
     }
     if constexpr (RP::n0) {
       xch_tile<SPLIT, RP::pO, 0>(w, s_tile, s_half, t);
-      apply_nibble<0, KIND>(w, R2, kTileBits);
+      apply_nibble<0, KIND, qm(0)>(w, R2, kTileBits);
     }
     if constexpr (RP::nIO) {
       xch_tile<SPLIT, RP::p0, RP::IO>(w, s_tile, s_half, t);
-      apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO)>(w, R2, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(w, s_tile, s_half, t);
     if constexpr (kRho) rho_apply(LIO{}, kTileBits, w, R2);
@@ -1021,18 +1054,18 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     static_assert(SPLIT, "co-traversed dual pass: half-tile re-layouts");
     if constexpr (RP::nO) {
       exchange_split2<RP::d_lay, RP::O>(v, w, s_half, s_half2, t);
-      apply_nibble<RP::O, KIND>(v, R, kTileBits);
-      apply_nibble<RP::O, KIND>(w, R2, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O)>(w, R2, kTileBits);
     }
     if constexpr (RP::n0) {
       exchange_split2<RP::pO, 0>(v, w, s_half, s_half2, t);
-      apply_nibble<0, KIND>(v, R, kTileBits);
-      apply_nibble<0, KIND>(w, R2, kTileBits);
+      apply_nibble<0, KIND, qm(0)>(v, R, kTileBits);
+      apply_nibble<0, KIND, qm(0)>(w, R2, kTileBits);
     }
     if constexpr (RP::nIO) {
       exchange_split2<RP::p0, RP::IO>(v, w, s_half, s_half2, t);
-      apply_nibble<RP::IO, KIND>(v, R, kTileBits);
-      apply_nibble<RP::IO, KIND>(w, R2, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO)>(w, R2, kTileBits);
     }
     exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t);
     if constexpr (kRho) {
@@ -1044,19 +1077,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::d_lay, RP::O>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(LO{}, sc);
-      apply_nibble<RP::O, KIND>(v, R, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(RP::O, kTileBits);
     }
     if constexpr (RP::n0) {
       xch_tile<SPLIT, RP::pO, 0>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(L0{}, sc);
-      apply_nibble<0, KIND>(v, R, kTileBits);
+      apply_nibble<0, KIND, qm(0)>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(0, kTileBits);
     }
     if constexpr (RP::nIO) {
       xch_tile<SPLIT, RP::p0, RP::IO>(v, s_tile, s_half, t);
       if (x_post) measure_x_post(LIO{}, sc);
-      apply_nibble<RP::IO, KIND>(v, R, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(v, s_tile, s_half, t);
     if constexpr (kRho) rho_apply(LIO{}, kTileBits, v, R);
@@ -1178,9 +1211,9 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
 
 // Kernel symbols per pass shape so rocprofv3 traces separate them.
 #define DTC_DEFINE_PASS(NAME, SHAPE_EXPR)                                          \
-  template <int NIBS, int KIND, int MC>                                            \
+  template <int NIBS, int KIND, int MC, int GEO = kGeoStd>                         \
   __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
-    pass_body<SHAPE_EXPR, NIBS, KIND, MC>(A);                                      \
+    pass_body<SHAPE_EXPR, NIBS, KIND, MC, false, false, false, GEO>(A);           \
   }
 DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
 // the K-D-K at three workgroups per CU (half-LDS re-layouts, 168 VGPRs) for
@@ -1189,23 +1222,23 @@ DTC_DEFINE_PASS(dtc_kdk_pass, kShapeKDK)
 // 12-site probe passes (r3i: <7> 5.36 ms vs 6.10; the 8-site ones are 2 %
 // slower at three) and every per-site / energy pass (r3r: energy K-D-K 1.81 ->
 // 1.69 ms at B=256, C4 +1 %)
-template <int NIBS, int KIND, int MC>
+template <int NIBS, int KIND, int MC, int GEO = kGeoStd>
 __global__ __launch_bounds__(kThreads, 3) void dtc_kdk_pass3(PassArgs A) {
-  pass_body<kShapeKDK, NIBS, KIND, MC, false, true>(A);
+  pass_body<kShapeKDK, NIBS, KIND, MC, false, true, false, GEO>(A);
 }
 // a forward K-D-K that also starts an echo branch (pass_body DUAL): two
 // tiles in registers, so two workgroups per CU; half-tile re-layouts (their
 // opaque per-thread bases keep the addresses out of the register budget: with
 // full-tile ones the <7> form takes 256 VGPRs and spills 27, r4u: 9.9 -> 11.5 ms)
-template <int NIBS, int KIND, int MC>
+template <int NIBS, int KIND, int MC, int GEO = kGeoStd>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kdk_dual(PassArgs A) {
-  pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true>(A);
+  pass_body<kShapeKDK, NIBS, KIND, MC, false, true, true, GEO>(A);
 }
 // its device-noise form: the forward K-D closing a period (device-like noise
 // runs no forward layer ahead) that also starts the echo branch
-template <int NIBS, int KIND, int MC>
+template <int NIBS, int KIND, int MC, int GEO = kGeoStd>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kd_dual(PassArgs A) {
-  pass_body<kShapeKD, NIBS, KIND, MC, false, true, true>(A);
+  pass_body<kShapeKD, NIBS, KIND, MC, false, true, true, GEO>(A);
 }
 DTC_DEFINE_PASS(dtc_kd_pass, kShapeKD)
 DTC_DEFINE_PASS(dtc_dk_pass, kShapeDK)
@@ -1214,9 +1247,9 @@ DTC_DEFINE_PASS(dtc_kick_pass, kShapeK)
 // The last pass of an echo chain: same work, probe measurement, no stores
 // (the echo state is never read again): 16 B of HBM traffic per amplitude.
 #define DTC_DEFINE_FINAL(NAME, SHAPE_EXPR)                                         \
-  template <int NIBS, int KIND>                                                    \
+  template <int NIBS, int KIND, int GEO = kGeoStd>                                 \
   __global__ __launch_bounds__(kThreads, 2) void NAME(PassArgs A) {                \
-    pass_body<SHAPE_EXPR, NIBS, KIND, 1, true>(A);                                 \
+    pass_body<SHAPE_EXPR, NIBS, KIND, 1, true, false, false, GEO>(A);             \
   }
 DTC_DEFINE_FINAL(dtc_kdk_final, kShapeKDK)
 DTC_DEFINE_FINAL(dtc_kd_final, kShapeKD)
@@ -1225,9 +1258,9 @@ DTC_DEFINE_FINAL(dtc_dk_final, kShapeDK)
 // per CU with the half-tile re-layouts: a read-only pass has no stores to
 // overlap its loads with, so the third workgroup's loads do (r4zc: C3's
 // <7> 3.80 -> 3.03 ms, <6> 3.24 -> 2.85 ms)
-template <int NIBS, int KIND>
+template <int NIBS, int KIND, int GEO = kGeoStd>
 __global__ __launch_bounds__(kThreads, 3) void dtc_kick_final(PassArgs A) {
-  pass_body<kShapeK, NIBS, KIND, 1, true, true>(A);
+  pass_body<kShapeK, NIBS, KIND, 1, true, true, false, GEO>(A);
 }
 #undef DTC_DEFINE_FINAL
 // The energy sweep's last pass (one kick layer past the last period, for the
@@ -1236,12 +1269,12 @@ template <int NIBS, int KIND>
 __global__ __launch_bounds__(kThreads, 2) void dtc_kick_xfinal(PassArgs A) {
   pass_body<kShapeK, NIBS, KIND, 3, true>(A);
 }
-template <int NIBS, int MC>
+template <int NIBS, int MC, int GEO = kGeoStd>
 __global__ __launch_bounds__(kThreads, 2) void dtc_diag_pass(PassArgs A) {
-  pass_body<kShapeD, NIBS, kKindRX, MC>(A);
+  pass_body<kShapeD, NIBS, kKindRX, MC, false, false, false, GEO>(A);
 }
 
-template <int NIBS, int KIND, int MC>
+template <int NIBS, int KIND, int MC, int GEO = kGeoStd>
 hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t stream) {
   dim3 block(kThreads);
   if (a.no_store) {
@@ -1253,10 +1286,10 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
       return hipErrorInvalidValue;  // probe passes end an echo chain, energy sweeps a kick pass
     } else {
       switch (shape) {
-        case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
-        case kShapeKD: hipLaunchKernelGGL((dtc_kd_final<NIBS, KIND>), grid, block, 0, stream, a); break;
-        case kShapeDK: hipLaunchKernelGGL((dtc_dk_final<NIBS, KIND>), grid, block, 0, stream, a); break;
-        case kShapeK: hipLaunchKernelGGL((dtc_kick_final<NIBS, KIND>), grid, block, 0, stream, a); break;
+        case kShapeKDK: hipLaunchKernelGGL((dtc_kdk_final<NIBS, KIND, GEO>), grid, block, 0, stream, a); break;
+        case kShapeKD: hipLaunchKernelGGL((dtc_kd_final<NIBS, KIND, GEO>), grid, block, 0, stream, a); break;
+        case kShapeDK: hipLaunchKernelGGL((dtc_dk_final<NIBS, KIND, GEO>), grid, block, 0, stream, a); break;
+        case kShapeK: hipLaunchKernelGGL((dtc_kick_final<NIBS, KIND, GEO>), grid, block, 0, stream, a); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1266,11 +1299,11 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     // K-D-K: unitary kicks; K-D: device-like noise (factored or general kicks)
     if constexpr (MC <= 1) {
       if (shape == kShapeKDK) {
-        hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
+        hipLaunchKernelGGL((dtc_kdk_dual<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a);
         return hipGetLastError();
       }
     }
-    if constexpr (MC <= 1 && (KIND == kKindRXU || KIND == kKindRYU || KIND == kKindGen)) {
+    if constexpr (MC <= 1 && GEO == kGeoStd && (KIND == kKindRXU || KIND == kKindRYU || KIND == kKindGen)) {
       if (shape == kShapeKD) {
         hipLaunchKernelGGL((dtc_kd_dual<NIBS, KIND, MC>), grid, block, 0, stream, a);
         return hipGetLastError();
@@ -1282,20 +1315,20 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
     case kShapeKDK:
       if constexpr (true) {
         if ((a.kdk_split >> (NIBS + (MC >= 2 ? 8 : 0))) & 1) {
-          hipLaunchKernelGGL((dtc_kdk_pass3<NIBS, KIND, MC>), grid, block, 0, stream, a);
+          hipLaunchKernelGGL((dtc_kdk_pass3<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a);
           break;
         }
       }
-      hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((dtc_kdk_pass<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a);
       break;
-    case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
-    case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
-    case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND, MC>), grid, block, 0, stream, a); break;
+    case kShapeKD: hipLaunchKernelGGL((dtc_kd_pass<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a); break;
+    case kShapeDK: hipLaunchKernelGGL((dtc_dk_pass<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a); break;
+    case kShapeK: hipLaunchKernelGGL((dtc_kick_pass<NIBS, KIND, MC, GEO>), grid, block, 0, stream, a); break;
     case kShapeD:
       if constexpr (MC == 3) {
         return hipErrorInvalidValue;  // no kicks: no X point
       } else {
-        hipLaunchKernelGGL((dtc_diag_pass<NIBS, MC>), grid, block, 0, stream, a);
+        hipLaunchKernelGGL((dtc_diag_pass<NIBS, MC, GEO>), grid, block, 0, stream, a);
       }
       break;
     default: return hipErrorInvalidValue;
@@ -1306,6 +1339,17 @@ hipError_t launch_shape(const PassArgs& a, dim3 grid, int shape, hipStream_t str
 template <int NIBS, int MC>
 hipError_t launch_kind_mc(const PassArgs& a, dim3 grid, int shape, int kind,
                           hipStream_t stream) {
+  if constexpr (NIBS == 6 && MC <= 1) {
+    // the 7-site column group of the 13 / 7 split (kGeoB7)
+    if (a.c == kB7Cols) {
+      if (a.s != 13 || a.act != 0xFE0) return hipErrorInvalidValue;
+      switch (kind) {
+        case kKindRX: return launch_shape<NIBS, kKindRX, MC, kGeoB7>(a, grid, shape, stream);
+        case kKindRY: return launch_shape<NIBS, kKindRY, MC, kGeoB7>(a, grid, shape, stream);
+        default: return hipErrorInvalidValue;
+      }
+    }
+  }
   switch (kind) {
     case kKindRX: return launch_shape<NIBS, kKindRX, MC>(a, grid, shape, stream);
     case kKindRY: return launch_shape<NIBS, kKindRY, MC>(a, grid, shape, stream);
@@ -1337,6 +1381,7 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, int mc
 
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream,
                        int* lc_variant) {
+  if (a.tile_bits == kMaxTileBits && shape != kShapeLC) return launch_pass13(a, batch, shape, kind, stream);
   if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch || batch > 65535 ||
       a.n_chunks > kMaxChunks)
     return hipErrorInvalidValue;

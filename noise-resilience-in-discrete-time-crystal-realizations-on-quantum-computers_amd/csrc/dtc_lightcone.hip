@@ -12,6 +12,13 @@
 
 // dtc_lcw2_final: workgroups per CU (its 38.7 KB of LDS allow four; four cap
 // the kernel at 128 VGPRs, three at 168)
+#ifndef DTC_LCW3_WPS
+#ifdef DTC_LCW3_ADD
+#define DTC_LCW3_WPS 3  // 41.2 KB of LDS with the padded additive slots
+#else
+#define DTC_LCW3_WPS 4
+#endif
+#endif
 #ifndef DTC_LCW2_WPS
 #define DTC_LCW2_WPS 4
 #endif
@@ -592,17 +599,6 @@ __device__ __forceinline__ int tab_base(int t, int bit_p5) {
 }
 }  // namespace lcw2
 
-// register bit Q <-> lane bit 4 (M = 16) or 5 (M = 32), for the whole tile
-template <int Q, int M>
-__device__ __forceinline__ void swap_reg_lane(double2 (&v)[kRegs]) {
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) {
-    if (r & (1 << Q)) continue;
-    swap_rows<M>(v[r].x, v[r | (1 << Q)].x);
-    swap_rows<M>(v[r].y, v[r | (1 << Q)].y);
-  }
-}
-
 template <int KIND>
 __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArgs A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
@@ -851,20 +847,50 @@ __global__ __launch_bounds__(kThreads, DTC_LCW2_WPS) void dtc_lcw2_final(PassArg
 // 41 site kicks, three LDS re-layouts, six row swaps (a seventh, swapping
 // m4 m3 back in X2, cost 1.7 % of the pass: r4m).  Re-layout slots are
 // the tile index mapped by an invertible GF(2) matrix (lcw3::cv: 4096 slots,
-// the thread's base XOR a compile-time register part): the low five bits of
-// the lane sites' vectors are independent in every layout written (lanes 0..3)
-// and read (lanes 0..4), so the accesses are conflict-free.  The cone
+// the thread's base XOR a compile-time register part): the low four bits of
+// the lane 0..3 sites' vectors are independent in every layout written, the
+// low five of lanes 0..4 in every layout read, so the accesses are
+// conflict-free (ds_write_b64: 16-lane groups, ds_read_b64: 32).  The cone
 // diagonals r = 6, 5, 4, 3 are split at j (two tables each, 456 entries with
 // r = 2 and 1; the r = 6 left table staged for the workgroup's bit j-6 only):
 // 40.1 KB of LDS, four workgroups per CU.
 namespace lcw3 {
 enum : int { m5 = 0, m4, m3, m2, m1, z0, p1, p2, p3, p4, p5, p6, kNSite };
 __host__ __device__ constexpr int off_of(int s) { return s - z0; }
+#ifdef DTC_LCW3_ADD
+// Development variant (round 6): additive slots, so a slot is the thread's
+// base plus a compile-time register part -- the ds_write_b64 / ds_read_b64
+// immediate, no address VALU per access.  Site -> position k of the padded
+// index y + (y >> 5) + (y >> 10) (strictly increasing in y: injective, 4226
+// slots); position k weighs 2^k + 2^(k-5) [k >= 5] + 2^(k-10) [k >= 10], so
+// its 2-adic valuation is k mod 5, and every layout's lane sites 0..4 (reads)
+// carry distinct valuations below 5 (the writes' lane 0..3 sites would need
+// distinct ones below 4: this variant leaves some writes two-way).
+__host__ __device__ constexpr int pos_of_site(int s) {
+  return s == m4 ? 0 : s == m3 ? 1 : s == m2 ? 2 : s == m1 ? 3 : s == z0 ? 4 : s == p3 ? 5
+       : s == p1 ? 6 : s == p5 ? 7 : s == p6 ? 8 : s == p2 ? 9 : s == m5 ? 10 : 11;
+}
 __host__ __device__ constexpr int cv(int s) {
-  return s == m4 ? 1 : s == m3 ? 2 : s == m2 ? 4 : s == m1 ? 8 : s == z0 ? 16
-       : s == p3 ? 32 | 1 : s == p4 ? 64 | 2 : s == p1 ? 128 | 2 : s == p5 ? 256 | 4
+  return (1 << pos_of_site(s)) + (pos_of_site(s) >= 5 ? 1 << (pos_of_site(s) - 5) : 0) +
+         (pos_of_site(s) >= 10 ? 1 << (pos_of_site(s) - 10) : 0);
+}
+static constexpr int kSlots = 4226;
+#define LCW3_SLOT(a, b) ((a) + (b))
+#else
+// (ds_write_b64 serves 16 contiguous lanes per LDS cycle: bank = slot mod 16;
+// ds_read_b64 32: slot mod 32.  The low four bits of the written layouts'
+// lane 0..3 sites and the low five of the read layouts' lane 0..4 sites are
+// independent -- checked by simulating the lane groups.  Round 6: z0's vector
+// had no low-four bits (16), so X3e's writes were two-way, 128 conflict cycles
+// per wave of the 276 SQ_LDS_BANK_CONFLICT counted, r6c)
+__host__ __device__ constexpr int cv(int s) {
+  return s == m4 ? 1 : s == m3 ? 2 : s == m2 ? 4 : s == m1 ? 8 : s == z0 ? 16 | 1
+       : s == p3 ? 32 | 2 : s == p4 ? 64 | 1 : s == p1 ? 128 | 2 : s == p5 ? 256 | 14
        : s == p6 ? 512 | 8 : s == p2 ? 1024 | 16 : 2048;
 }
+static constexpr int kSlots = kTile;
+#define LCW3_SLOT(a, b) ((a) ^ (b))
+#endif
 // layouts: positions 0..3 registers, 4..9 lane bits 0..5, 10..11 wave bits
 enum : int { kX1 = 0, kX1e, kX1f, kX2, kX2s, kX3, kX3e, kX4, kX4e };
 __host__ __device__ constexpr int lay_site(int li, int pos) {
@@ -881,14 +907,16 @@ __host__ __device__ constexpr int lay_site(int li, int pos) {
   return tab[li][pos];
 }
 __host__ __device__ constexpr int reg_slot(int li, int r) {
-  return ((r & 1) ? cv(lay_site(li, 0)) : 0) ^ ((r & 2) ? cv(lay_site(li, 1)) : 0) ^
-         ((r & 4) ? cv(lay_site(li, 2)) : 0) ^ ((r & 8) ? cv(lay_site(li, 3)) : 0);
+  return LCW3_SLOT(LCW3_SLOT(LCW3_SLOT((r & 1) ? cv(lay_site(li, 0)) : 0,
+                                       (r & 2) ? cv(lay_site(li, 1)) : 0),
+                             (r & 4) ? cv(lay_site(li, 2)) : 0),
+                   (r & 8) ? cv(lay_site(li, 3)) : 0);
 }
 template <int LI>
 __device__ __forceinline__ int slot_base(int t) {
   int b = 0;
 #pragma unroll
-  for (int p = 4; p < 12; ++p) b ^= ((t >> (p - 4)) & 1) * cv(lay_site(LI, p));
+  for (int p = 4; p < 12; ++p) b = LCW3_SLOT(b, ((t >> (p - 4)) & 1) * cv(lay_site(LI, p)));
   return b;
 }
 // cone tables in LDS (double2 entries), natural index order from bit lo
@@ -934,10 +962,10 @@ __device__ __forceinline__ int tab_base(int t) {
 }  // namespace lcw3
 
 template <int KIND>
-__global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
+__global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArgs A) {
   static_assert(KIND == kKindRX || KIND == kKindRY, "light-cone pass: factored kicks");
   using namespace lcw3;
-  __shared__ double s_x[kTile];
+  __shared__ double s_x[kSlots];
   __shared__ double2 s_tab[kTabEntries];
   __shared__ double s_red[kThreads / 64][2];
   const int t = threadIdx.x;
@@ -963,16 +991,16 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
     int bf = slot_base<F>(t), bt = slot_base<T>(t);
     asm volatile("" : "+v"(bf), "+v"(bt));
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) s_x[bf ^ reg_slot(F, r)] = v[r].x;
+    for (int r = 0; r < kRegs; ++r) s_x[LCW3_SLOT(bf, reg_slot(F, r))] = v[r].x;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r].x = s_x[bt ^ reg_slot(T, r)];
+    for (int r = 0; r < kRegs; ++r) v[r].x = s_x[LCW3_SLOT(bt, reg_slot(T, r))];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) s_x[bf ^ reg_slot(F, r)] = v[r].y;
+    for (int r = 0; r < kRegs; ++r) s_x[LCW3_SLOT(bf, reg_slot(F, r))] = v[r].y;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r].y = s_x[bt ^ reg_slot(T, r)];
+    for (int r = 0; r < kRegs; ++r) v[r].y = s_x[LCW3_SLOT(bt, reg_slot(T, r))];
   };
   auto kick = [&](auto q_tag, auto l_tag, auto s_tag) {
     constexpr int Q = decltype(q_tag)::value, l = decltype(l_tag)::value, S = decltype(s_tag)::value;
@@ -1095,7 +1123,9 @@ __global__ __launch_bounds__(kThreads, 4) void dtc_lcw3_final(PassArgs A) {
   kick(C2{}, C0{}, LCW3_S(p5));
   kick(C3{}, C0{}, LCW3_S(p6));
   swap_reg_lane<3, 16>(v);  // register bit 3: p2 (lane bit 4: p6)
-  kick(C3{}, C0{}, LCW3_S(p2));
+  // (the 13 / 7 split's chains start with group B = sites j+3 ..: no p2 kick
+  // in l0; workgroup-uniform)
+  if ((A.lc_mask >> p2) & 1ull) kick(C3{}, C0{}, LCW3_S(p2));
   // stage the tables at their frame-masked slots, conjugated for D*
   {
     const double cs = A.diag_conj ? -1.0 : 1.0;

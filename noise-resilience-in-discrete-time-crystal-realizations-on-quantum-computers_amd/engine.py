@@ -424,11 +424,12 @@ class DtcEngine:
     def schedule_counts(self):
         """Batch schedules built since the engine opened (dtc_schedule_counts):
         echo chains folded into a dual pass, device-noise batches whose forward
-        ran a layer ahead, and device-noise batches run with K-D forward passes
-        (a chain did not fold, or DTC_NO_RUNAHEAD=1)."""
-        c = (ctypes.c_int64 * 3)()
+        ran a layer ahead, device-noise batches run with K-D forward passes
+        (a chain did not fold, or DTC_NO_RUNAHEAD=1), and batches run with the
+        13 / 7 site split of L = 20."""
+        c = (ctypes.c_int64 * 4)()
         _capi.check(self._lib.dtc_schedule_counts(self._ctx, c))
-        return {"folded": c[0], "device_runahead": c[1], "device_kd": c[2]}
+        return {"folded": c[0], "device_runahead": c[1], "device_kd": c[2], "split13": c[3]}
 
     def device_info(self):
         name = ctypes.create_string_buffer(256)

@@ -286,7 +286,7 @@ def test_device_dual_pass(pkg, monkeypatch, L, T, state, pol, toff):
         assert cnt["device_kd"] == 0 and cnt["device_runahead"] == 1 and cnt["folded"] > 0, cnt
     else:
         assert cnt["device_kd"] == 1 and cnt["device_runahead"] == 0 and cnt["folded"] > 0, cnt
-    assert cnt_ref == {"folded": 0, "device_runahead": 0, "device_kd": 1}, cnt_ref
+    assert cnt_ref == {"folded": 0, "device_runahead": 0, "device_kd": 1, "split13": 0}, cnt_ref
 
 
 @pytest.mark.parametrize("L,T,pol", [(14, 6, "x"), (20, 5, "circular_left")])

@@ -15,8 +15,8 @@ for setting in "$@"; do
 import json, sys, pandas as pd
 d = json.load(open(sys.argv[1] + ".json"))
 k = pd.read_csv(sys.argv[1] + "/kt_kernel_stats.csv")
-k = k[k.Name.str.contains("kdk")]
+k = k[k.Name.str.contains("kdk|pass13|lcw3")]
 print(sys.argv[2], round(d["value"]), round(d["roofline"]["achieved"]),
-      " ".join(f"{r.Name.split('<')[1].split('>')[0].replace(' ', '')}={r.AverageNs / 1e6:.4f}" for r in k.itertuples()))
+      " ".join(f"{r.Name.split('dtc_')[-1].split('(')[0].replace(' ', '')}={r.AverageNs / 1e6:.4f}x{r.Calls}" for r in k.itertuples()))
 PY
 done

@@ -14,7 +14,8 @@ git show $REV:include/dtc.h > $T/include/dtc.h
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17"
 (cd $T/a/csrc && { /opt/rocm/bin/hipcc $F -c dtc_kernels.hip -o $T/k.o 2>/dev/null &
                    /opt/rocm/bin/hipcc $F -c dtc_lightcone.hip -o $T/l.o 2>/dev/null &
+                 /opt/rocm/bin/hipcc $F -c dtc_tile13.hip -o $T/t.o 2>/dev/null &
                    /opt/rocm/bin/hipcc $F -c dtc_engine.cpp -o $T/e.o; wait; })
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared $T/k.o $T/l.o $T/e.o -o devlib/$NAME.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared $T/k.o $T/l.o $T/t.o $T/e.o -o devlib/$NAME.so
 rm -rf $T
 echo devlib/$NAME.so

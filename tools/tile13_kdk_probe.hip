@@ -156,10 +156,14 @@ __device__ __forceinline__ void kdk_probe(double2* __restrict__ st, int og, int 
     kicks(K4{}); xch(P_(9), P_(5)); kicks(K3{});
     diag();
     kicks(K3{}); xch(P_(5), P_(9)); kicks(K4{});
-  } else {  // B13c5 (round 6): 8 sites 12..19 over 512-B columns: IO 9 (sites 16..19) -> 5 (12..15) | D | back
+  } else if constexpr (PROG == 4) {  // B13c5 (round 6): 8 sites 12..19 over 512-B columns: IO 9 (sites 16..19) -> 5 (12..15) | D | back
     kicks(K4{}); xch(P_(9), P_(5)); kicks(K4{});
     diag();
     kicks(K4{}); xch(P_(5), P_(9)); kicks(K4{});
+  } else {  // B12c5 (round 6): 12-bit tile, 7 sites 13..19 over 512-B columns: IO 8 (16..19) -> 4 (col 4, 13..15) | D | back
+    kicks(K4{}); xch(P_(8), P_(4)); kicks(K3{});
+    diag();
+    kicks(K3{}); xch(P_(4), P_(8)); kicks(K4{});
   }
 #undef P_
 #pragma unroll
@@ -230,6 +234,10 @@ int main(int argc, char** argv) {
     RUN("B13c5 c=5 s=12 (8 sites), half-tile LDS, 2 WG/CU", 13, 5, true, 9, 4, 2);
     RUN("B13c5 c=5 s=12 (8 sites), full-tile LDS, 1 WG/CU", 13, 5, false, 9, 4, 1);
     RUN("B12 c=4 s=12, half-tile LDS, 3 WG/CU", 12, 4, true, 8, 1, 3);
+    // round 6: the 13/7 split's column pass on a 12-bit tile (7 sites + 5
+    // column bits: 512-B runs): is the gain the site count or the 1 KiB runs?
+    RUN("B12c5 c=5 s=13 (7 sites), full-tile LDS, 2 WG/CU", 12, 5, false, 8, 5, 2);
+    RUN("B12c5 c=5 s=13 (7 sites), half-tile LDS, 3 WG/CU", 12, 5, true, 8, 5, 3);
   }
   return 0;
 }
