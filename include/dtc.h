@@ -346,7 +346,8 @@ int dtc_lightcone_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
  * forward passes (a chain did not fold, or DTC_NO_RUNAHEAD=1, the test switch
  * that forces this schedule; two passes per period), [3] batches run with the
  * 13 / 7 site split of L = 20 (a 13-site group in 8192-amplitude tiles, a
- * 7-site column group; DTC_NO_SPLIT13=1 keeps the 12 / 8 split). */
+ * 7-site column group; opt-in with DTC_SPLIT13=1, the default keeps the
+ * 12 / 8 split). */
 int dtc_schedule_counts(dtc_ctx* ctx, int64_t* counts /* [4] */);
 
 /* Device properties for reports. */

@@ -123,7 +123,10 @@ struct dtc_ctx {
   int64_t lc_launches[4] = {};  // light-cone passes by kernel (dtc_lightcone_counts)
   bool dual = true;  // DTC_NO_DUAL: echo chains start with a pass of their own
   bool runahead = true;  // DTC_NO_RUNAHEAD: device-noise forward closes periods with K-D
-  bool split13 = true;   // DTC_NO_SPLIT13: L = 20 sweeps keep the 12 / 8 site groups
+  // DTC_SPLIT13=1: L = 20 sweeps run the 13 / 7 site groups (round 6: built
+  // and parity-tested, slower than the 12 / 8 split on the power-capped chip,
+  // profiles/r6q_*; the 12 / 8 split stays the default)
+  bool split13 = false;
   int64_t sched_counts[4] = {};  // dtc_schedule_counts: folds, run-ahead, rebuilt, 13 / 7
   double st_ms[DTC_KERNEL_KINDS] = {};
   double st_bytes[DTC_KERNEL_KINDS] = {};
@@ -651,6 +654,11 @@ int launch_pass_spec(dtc_ctx* ctx, const RunCfg& rc, int64_t batch_start, int ba
   A.act = g.act;
   A.recs = recs;
   A.diag_conj = ps.diag == dtc::kDiagConj;
+#ifdef DTC_DEV_KNOBS
+  // development builds, timing probes only (wrong results): DTC_DBG_CONJ=0 / 1
+  // runs every diagonal unconjugated / conjugated
+  if (const char* e = std::getenv("DTC_DBG_CONJ")) A.diag_conj = std::atoi(e) != 0;
+#endif
   A.meas = meas_mode;
   A.meas_at_end = meas_at_end;
   A.meas_parts = meas_parts;
@@ -1335,7 +1343,7 @@ int dtc_open(int32_t device, dtc_ctx** out) {
   c->lc_wide3 = c->lc_wide && std::getenv("DTC_NO_LCW3") == nullptr;
   c->dual = std::getenv("DTC_NO_DUAL") == nullptr;
   c->runahead = std::getenv("DTC_NO_RUNAHEAD") == nullptr;
-  c->split13 = std::getenv("DTC_NO_SPLIT13") == nullptr;
+  if (const char* e = std::getenv("DTC_SPLIT13")) c->split13 = std::atoi(e) != 0;
   c->verbose = std::getenv("DTC_VERBOSE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1647,6 +1655,11 @@ int autocorr_impl(dtc_ctx* ctx, const dtc_problem* pr, const dtc_noise* nz,
     }
     double2* F = (double2*)ctx->F.p;
     double2* E = (double2*)ctx->E.p;
+#ifdef DTC_DEV_KNOBS
+    // development builds: DTC_FE_SWAP=1 runs the forward in the echo buffer and
+    // the echo chains in the forward buffer (buffer-placement A/B)
+    if (want_e && !use_prefix && std::getenv("DTC_FE_SWAP")) std::swap(F, E);
+#endif
     // the first forward pass reads the prefix states (or the basis states in F)
     // (bs is a multiple of 8 in the octet layout: the batch starts an octet)
     const double2* F0 = use_prefix ? (const double2*)ctx->prefix.p + (size_t)bs * pl.len : F;

@@ -177,6 +177,11 @@ union KickRec {
 static constexpr int kMaxTileBits = 13;
 static constexpr int kRecPerState = 2 * kMaxTileBits + 1;
 static constexpr int kRecTotal = 2 * kTileBits;
+// 13-site passes (Pauli-frame records, dtc_kernels.hip frame13_records): every
+// kick record holds the signed form-B coefficient; the total record (26) adds
+// the X masks the four re-layouts flush (tile bits) and the Z mask of the
+// diagonal
+enum : int { kT13MaskX1 = 3, kT13MaskX2 = 4, kT13MaskX3 = 5, kT13MaskX4 = 6, kT13MaskZ = 7 };
 
 // One pass's kick layers, as the prep kernel needs them.
 struct PassKick {

@@ -233,6 +233,82 @@ __device__ __forceinline__ void canonicalise(int kind, const double2* m, SiteMat
   sm.var = (form_b ? 2 : 0) | (neg ? 1 : 0);
 }
 
+// Pauli-frame records of a 13-site pass (dtc_tile13.hip).  The pass runs one
+// butterfly for every kick, the form-B one G(f) (RX: f I + i X; RY: f I + i Y),
+// so its kicks carry no variant branches (the 128-VGPR budget of the 13-bit
+// tile spilled at the four-way branches, r6d).  The other forms become Paulis:
+// form A is A(beta) = -i X G(-beta) (RX) or X Z G(-beta) (RY), sigma = -1 is
+// a Z after the kick.  The true state is i^ph X^x Z^z (the computed state);
+// a kick M = i^k' Z^n X^a G(g) on site q is run as G(+-g) (G past the frame:
+// RX flips g and the sign on Z_q; RY on X_q xor Z_q), and the frame takes
+// Z^n X^a.  X bits are flushed by the re-layouts (the LDS write slot of tile
+// index y becomes slot(y ^ m): the tile comes out X^m-permuted), Z bits by the
+// diagonal (a sign per amplitude, folded into its tables): masks chosen so the
+// frame is the identity at the diagonal and at the store, the X of a kick that
+// has no re-layout after it taken before it (pre-flushed; RX commutes it, RY
+// flips g).  Kick order of the kernel: pre 4..8 | x1 | 0..3 | x2 | 9..12 | D
+// | post 9..12 | x3 | 0..3 | x4 | 8, 4..7.  Writes f (d[0]) and variant 2 into
+// the kick records, the masks into tot (kT13Mask*); returns the extra power of
+// i.  The algebra is restated in numpy and checked against the direct 2x2
+// products by tests/test_frame13_model.py.
+__device__ int frame13_records(const PassKick& pk, KickRec* out, const int* fvar, KickRec& tot) {
+  constexpr int NB = kMaxTileBits;
+  const bool rx = pk.kind == kKindRX;
+  int x = 0, z = 0, ph = 0;
+  auto form_a = [&](int i) { return (fvar[i] >> 1) ^ 1; };
+  auto zbit = [&](int i) { return rx ? (fvar[i] & 1) : ((fvar[i] & 1) ^ form_a(i)); };
+  auto kick = [&](int h, int q) {
+    const int i = h * NB + q;
+    const int fa = form_a(i), n2 = zbit(i);
+    const double g = fa ? -out[i].d[0] : out[i].d[0];
+    const int flip = ((rx ? z : (x ^ z)) >> q) & 1;
+    out[i].d[0] = flip ? -g : g;
+    out[i].i[1] = 2;
+    ph += (rx ? 3 * fa : 2 * fa) + 2 * flip;
+    x ^= fa << q;
+    ph += 2 * (n2 & (x >> q) & 1);
+    z ^= n2 << q;
+  };
+  auto flush_x = [&](int m) {
+    ph += 2 * (__popc(z & m) & 1);
+    x ^= m;
+    return m;
+  };
+  const bool pre = pk.pre.enabled, post = pk.post.enabled;
+  auto xbits = [&](int h, int q0, int q1) {
+    int m = 0;
+    for (int q = q0; q <= q1; ++q) m |= form_a(h * NB + q) << q;
+    return m;
+  };
+  int m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+  if (pre) {
+    for (int q = 4; q <= 8; ++q) kick(0, q);
+    m1 = flush_x(x);
+    for (int q = 0; q <= 3; ++q) kick(0, q);
+    m2 = flush_x(x ^ xbits(0, 9, 12));
+    for (int q = 9; q <= 12; ++q) kick(0, q);
+  }
+  int npost = 0;
+  if (post)
+    for (int q = 0; q < NB; ++q) npost |= zbit(NB + q) << q;
+  const int md = z ^ npost;
+  z ^= md;
+  if (post) {
+    for (int q = 9; q <= 12; ++q) kick(1, q);
+    m3 = flush_x(x);
+    for (int q = 0; q <= 3; ++q) kick(1, q);
+    m4 = flush_x(x ^ xbits(1, 4, 8));
+    kick(1, 8);
+    for (int q = 4; q <= 7; ++q) kick(1, q);
+  }
+  tot.i[kT13MaskX1] = m1;
+  tot.i[kT13MaskX2] = m2;
+  tot.i[kT13MaskX3] = m3;
+  tot.i[kT13MaskX4] = m4;
+  tot.i[kT13MaskZ] = md;
+  return ph;
+}
+
 // Kick records (dtc_kernels.h: KickRec) of n_pass passes x batch states: one
 // thread per (pass, state) builds the 24 noisy site kicks of the pass, writes
 // their factored forms and the product of their global factors.
@@ -361,6 +437,8 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   int ksum = 0;
   double w[2] = {1.0, 1.0};
   const int tb = pk.tb == kMaxTileBits ? kMaxTileBits : kTileBits;
+  const bool frame13 = tb == kMaxTileBits && (pk.kind == kKindRX || pk.kind == kKindRY);
+  int fvar[2 * kMaxTileBits];
   for (int half = 0; half < 2; ++half) {
     const KickDesc& K = half == 0 ? pk.pre : pk.post;
     for (int k = 0; k < tb; ++k) {
@@ -394,14 +472,16 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
         for (int e = 3; e < 8; ++e) r.d[e] = 0.0;
       }
       out[half * tb + k] = r;
+      if (frame13) fvar[half * tb + k] = sm.var;
       ksum += sm.k;
       w[half] *= sm.scale;
     }
   }
-  const int kph = ksum & 3;
-  const double wg = w[0] * w[1];
   KickRec tot;
   for (int e = 0; e < 8; ++e) tot.d[e] = 0.0;
+  if (frame13) ksum += frame13_records(pk, out, fvar, tot);
+  const int kph = ksum & 3;
+  const double wg = w[0] * w[1];
   tot.d[0] = kph == 0 ? wg : (kph == 2 ? -wg : 0.0);
   tot.d[1] = kph == 1 ? wg : (kph == 3 ? -wg : 0.0);
   tot.d[2] = 1.0 / (w[1] * w[1]);
@@ -1379,8 +1459,22 @@ hipError_t launch_kind(const PassArgs& a, dim3 grid, int shape, int kind, int mc
   }
 }
 
+#ifdef DTC_DEV_KNOBS
+__global__ void dbg_spacer_kernel(int us) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)us * 100) __builtin_amdgcn_s_sleep(10);
+}
+#endif
+
 hipError_t launch_pass(const PassArgs& a, int batch, int shape, int kind, hipStream_t stream,
                        int* lc_variant) {
+#ifdef DTC_DEV_KNOBS
+  // development builds, timing probe: DTC_DBG_SPACER=<us> runs a one-wave
+  // sleep kernel of that length before every 13-site pass
+  if (a.tile_bits == kMaxTileBits && shape != kShapeLC)
+    if (const char* e = std::getenv("DTC_DBG_SPACER"))
+      hipLaunchKernelGGL(dbg_spacer_kernel, dim3(1), dim3(64), 0, stream, std::atoi(e));
+#endif
   if (a.tile_bits == kMaxTileBits && shape != kShapeLC) return launch_pass13(a, batch, shape, kind, stream);
   if (a.L_eff > 32 || a.L_eff < kTileBits || a.batch != batch || batch > 65535 ||
       a.n_chunks > kMaxChunks)

@@ -72,12 +72,20 @@ __device__ __forceinline__ int ythr(int t) {
 // 1) << 4, made L0's writes two-way: 256 conflict cycles per wave, r6e).
 __host__ __device__ constexpr int slot(int y) { return y ^ ((y >> 4) & 31); }
 
-template <int FROM, int TO>
-__device__ __forceinline__ void xch(double2 (&v)[kRegs], double* s_half, int t) {
-  int bf = slot(ythr<FROM>(t)), bt = slot(ythr<TO>(t));
+template <int FROM, int TO, bool FIRST = false>
+__device__ __forceinline__ void xch(double2 (&v)[kRegs], double* s_half, int t, int xm = 0) {
+  // xm: the Pauli frame's X bits this re-layout flushes (frame13_records): the
+  // writes go to slot(y ^ xm) = slot(y) ^ slot(xm), so the tile comes out
+  // X^xm-permuted
+  int bf = slot(ythr<FROM>(t)) ^ slot(xm), bt = slot(ythr<TO>(t));
   asm volatile("" : "+v"(bf), "+v"(bt));
-  // (no barrier before the writes: a thread writes exactly the slots it read
-  // itself in the previous re-layout, which ended in layout FROM)
+  // no barrier before the writes when xm = 0: a thread writes exactly the
+  // slots it read itself in the previous re-layout (which ended in layout
+  // FROM); a flush writes other threads' slots, so it waits for their reads
+  // (FIRST: the pass's first re-layout, no reads before it)
+#ifndef DTC_T13_NOBAR_PROBE  // timing probe only (wrong results by design)
+  if (!FIRST && xm) __syncthreads();
+#endif
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) s_half[bf ^ slot(yreg(FROM, r))] = v[r].x;
   __syncthreads();
@@ -91,37 +99,11 @@ __device__ __forceinline__ void xch(double2 (&v)[kRegs], double* s_half, int t) 
   for (int r = 0; r < kRegs; ++r) v[r].y = s_half[bt ^ slot(yreg(TO, r))];
 }
 
-// one variant of a site kick over the tile's eight register pairs, each pair
-// updated in place: the empty asm pins the pair's results before the next
-// pair starts, so the four variant branches below merge without a copy of
-// the tile (unpinned, the compiler computed all 32 results of a branch into
-// fresh registers first: 64 more VGPRs, spills at 128)
-template <int KIND, int VAR, int Q>
-__device__ __forceinline__ void layer_pinned(double2 (&v)[kRegs], double f) {
-#pragma unroll
-  for (int r = 0; r < kRegs; ++r) {
-    if (r & (1 << Q)) continue;
-    double2& u = v[r];
-    double2& w = v[r | (1 << Q)];
-    if (KIND == kKindRX) bfly_rx_f<VAR>(u, w, f);
-    else bfly_ry_f<VAR>(u, w, f);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-// one site kick: register bit Q, record k (factored RX / RY family)
+// one site kick: register bit Q, record k -- the form-B butterfly with the
+// frame-signed coefficient (frame13_records), no variant branch
 template <int Q, int KIND, typename Rec>
 __device__ __forceinline__ void kick(double2 (&v)[kRegs], const Rec& R, int k) {
-  const double f = R.d(k, 0);
-#ifdef DTC_T13_VAR0_PROBE
-  // timing probe only (wrong results by design): the first variant always
-  layer_pinned<KIND, 0, Q>(v, f);
-  return;
-#endif
-  const int var = R.i(k, 1);
-  if (var == 0) layer_pinned<KIND, 0, Q>(v, f);
-  else if (var == 1) layer_pinned<KIND, 1, Q>(v, f);
-  else if (var == 2) layer_pinned<KIND, 2, Q>(v, f);
-  else layer_pinned<KIND, 3, Q>(v, f);
+  layer_f<KIND, 2, Q>(v, R.d(k, 0));
 }
 // the four register sites of layout LI (records rec0 + tile bit)
 template <int LI, int KIND, typename Rec>
@@ -199,10 +181,17 @@ __device__ __forceinline__ void pass13_body(const PassArgs& A) {
   }
   // vmcnt(16): records and tables landed, the tile's 16 loads in flight
   __builtin_amdgcn_s_waitcnt(0x4F70);
+  // the Pauli frame's Z flush (frame13_records), a sign per amplitude at the
+  // diagonal: tile bits 0..8 are L9's thread bits (zt), 9..12 its registers
+  const int zm = R.i(kRecTot, kT13MaskZ);
+  const bool zt = __builtin_popcount(ythr<L9>(t) & zm) & 1;
   if (DIAG) {
     const double cs = A.diag_conj ? -1.0 : 1.0;
     if (t < A.n_chunks * 64) s_chunk[t] = make_double2(dchunk.x, cs * dchunk.y);
-    if (t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    // the window entry of register bits (t >> 1) & 15 (tile bits 9..12) takes
+    // their share of the Z flush
+    const double zs = (__builtin_popcount((t >> 1) & (zm >> 9) & 15) & 1) ? -1.0 : 1.0;
+    if (t < 64) s_win[t] = make_double2(zs * dwin.x, zs * cs * dwin.y);
     // made visible by the first re-layout's barriers (every shape re-lays out
     // before its diagonal: L9 is not the load layout)
   }
@@ -246,25 +235,39 @@ __device__ __forceinline__ void pass13_body(const PassArgs& A) {
     kick4<LIO, KIND>(v, R, 0);
     swap_reg_lane<0, 16>(v);
     kick<0, KIND>(v, R, 8);
-    xch<LIOs, L0>(v, s_half, t);
+    xch<LIOs, L0, true>(v, s_half, t, R.i(kRecTot, kT13MaskX1));
     kick4<L0, KIND>(v, R, 0);
-    xch<L0, L9>(v, s_half, t);
+    xch<L0, L9>(v, s_half, t, R.i(kRecTot, kT13MaskX2));
     kick4<L9, KIND>(v, R, 0);
   } else if constexpr (DIAG) {
-    xch<LIO, L9>(v, s_half, t);
+    xch<LIO, L9, true>(v, s_half, t);
   }
   if constexpr (!DIAG) {
+    // the global factor and the Z flush (L9: register bits = tile bits 9..12)
+    const double2 g = zt ? make_double2(-gph.x, -gph.y) : gph;
+    const double2 gn = make_double2(-g.x, -g.y);
+    const int zr = (zm >> 9) & 15;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
+    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], (__builtin_popcount(r & zr) & 1) ? gn : g);
   } else {
     // D(x) = P_C * W[x]: P_C = D(x0) / W(x0) per thread, W indexed by bits
     // 8..13 of x (the 64-entry window table of start bit 9)
     const int64_t x0 = tbase | ythr<L9>(t);
     const int w0i = (int)(((x0 << 1) >> kG0) & 63);
     const double2 w0 = s_win[w0i];
-    const double2 pc = cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+    const double2 pc0 = cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)), gph);
+    const double2 pc = zt ? make_double2(-pc0.x, -pc0.y) : pc0;
+    // four window entries in flight at a time: all sixteen at once (64 VGPRs
+    // next to the tile's 64) spilled at the 128-VGPR budget; the empty asm
+    // (memory clobber) keeps the next group's reads below this group's products
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
+    for (int r0 = 0; r0 < kRegs; r0 += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[r0 + j] = cmul(v[r0 + j], cmul(pc, s_win[w0i | ((r0 + j) << 1)]));
+      asm volatile("" : "+v"(v[r0].x), "+v"(v[r0].y), "+v"(v[r0 + 1].x), "+v"(v[r0 + 1].y),
+                   "+v"(v[r0 + 2].x), "+v"(v[r0 + 2].y), "+v"(v[r0 + 3].x), "+v"(v[r0 + 3].y)
+                   :: "memory");
+    }
   }
   if constexpr (MC == 1) {
     if (A.meas != kMeasNone && !A.meas_at_end) {
@@ -275,9 +278,9 @@ __device__ __forceinline__ void pass13_body(const PassArgs& A) {
   // ---- post-kick: L9 9..12, L0 0..3, (LIOs) 8, swap back, LIO 4..7 ----
   if constexpr (POST) {
     kick4<L9, KIND>(v, R, kBits);
-    xch<L9, L0>(v, s_half, t);
+    xch<L9, L0>(v, s_half, t, R.i(kRecTot, kT13MaskX3));
     kick4<L0, KIND>(v, R, kBits);
-    xch<L0, LIOs>(v, s_half, t);
+    xch<L0, LIOs>(v, s_half, t, R.i(kRecTot, kT13MaskX4));
     kick<0, KIND>(v, R, kBits + 8);
     swap_reg_lane<0, 16>(v);
     kick4<LIO, KIND>(v, R, kBits);
@@ -371,7 +374,11 @@ hipError_t launch_pass13(const PassArgs& a, int batch, int shape, int kind, hipS
   const int n_tiles = 1 << (a.L_eff - kBits);
   if (a.octet_bits && (a.octet_bits < 4 || a.octet_bits > a.L_eff)) return hipErrorInvalidValue;
   const dim3 grid = a.octet_bits ? dim3(n_tiles * 8, (batch + 7) / 8) : dim3(n_tiles, batch);
+#ifdef DTC_T13_MC1_PROBE  // development A/B: the measuring instantiation for every pass
+  const int mc = 1;
+#else
   const int mc = a.meas == kMeasNone ? 0 : 1;
+#endif
   if (kind == kKindRX)
     return mc ? launch13_kind<kKindRX, 1>(a, grid, shape, stream)
               : launch13_kind<kKindRX, 0>(a, grid, shape, stream);

@@ -185,6 +185,35 @@ __global__ __launch_bounds__(1 << (TB - 4)) __attribute__((amdgpu_waves_per_eu(
   kdk_probe<TB, C, HALF, IOP, PROG>(st, og, batch, coefs, tabs, s_x, s_full, s_tab);
 }
 
+// round 6: state filled with normalised pseudo-random amplitudes (argv[3] =
+// "rand"): do the passes' times depend on the data (zeros vs dense values)?
+__global__ void fill_rand(double2* st, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = i * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 31;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 29;
+  const double a = (double)(h & 0xFFFFF) / 1048576.0 - 0.5, c = (double)((h >> 20) & 0xFFFFF) / 1048576.0 - 0.5;
+  st[i] = make_double2(a * 1e-3, c * 1e-3);
+}
+
+// round 6: what precedes a pass -- an idle gap (one sleeping wave) or a
+// VALU-heavy burner on every CU (FP64 FMA chains, no memory) of ~us microseconds
+__global__ void k_sleep(int us) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)us * 100) __builtin_amdgcn_s_sleep(10);
+}
+__global__ void k_burn(int us, double* sink) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  double a = threadIdx.x * 1e-3, b = 0.999, c = 1e-3;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)us * 100) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) a = fma(a, b, c);
+  }
+  if (a == 12345.0) sink[0] = a;
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 1024, og = 6;
   const size_t n = (size_t)B << 20;
@@ -193,10 +222,22 @@ int main(int argc, char** argv) {
   double2* tabs;
   CHECK(hipMalloc(&st, n * 16));
   CHECK(hipMemset(st, 0, n * 16));
+  if (argc > 3) {
+    hipLaunchKernelGGL(fill_rand, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, st, n);
+    CHECK(hipDeviceSynchronize());
+  }
   CHECK(hipMalloc(&coefs, 4096 * 8));
   CHECK(hipMemset(coefs, 0, 4096 * 8));
   CHECK(hipMalloc(&tabs, 256 * 16));
   CHECK(hipMemset(tabs, 0, 256 * 16));
+  if (argc > 3) {
+    double2 ht[256];
+    double hc[4096];
+    for (int i = 0; i < 256; ++i) ht[i] = make_double2(0.6, 0.8);
+    for (int i = 0; i < 4096; ++i) hc[i] = 0.05;
+    CHECK(hipMemcpy(tabs, ht, sizeof(ht), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(coefs, hc, sizeof(hc), hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -216,6 +257,73 @@ int main(int argc, char** argv) {
     printf("%-58s %8.3f ms  %7.0f GB/s\n", name, ms, n * 32.0 / (ms * 1e6));
     return 0;
   };
+  // round 6: two passes alternating (the product's chains alternate the row
+  // and the column group): each one's own time when it follows the other
+  hipEvent_t ev[41];
+  for (auto& evx : ev) CHECK(hipEventCreate(&evx));
+  auto pair = [&](const char* na, auto la, const char* nb, auto lb) -> int {
+    la();
+    lb();
+    CHECK(hipDeviceSynchronize());
+    for (int i = 0; i < 20; ++i) {
+      CHECK(hipEventRecord(ev[2 * i]));
+      la();
+      CHECK(hipEventRecord(ev[2 * i + 1]));
+      lb();
+    }
+    CHECK(hipEventRecord(ev[40]));
+    CHECK(hipEventSynchronize(ev[40]));
+    float ta = 0, tb = 0;
+    for (int i = 0; i < 20; ++i) {
+      float x = 0, y = 0;
+      CHECK(hipEventElapsedTime(&x, ev[2 * i], ev[2 * i + 1]));
+      CHECK(hipEventElapsedTime(&y, ev[2 * i + 1], ev[2 * i + 2]));
+      ta += x / 20;
+      tb += y / 20;
+    }
+    printf("alternating: %-34s %8.3f ms | %-34s %8.3f ms\n", na, ta, nb, tb);
+    return 0;
+  };
+#define LNCH(TB, C, HALF, IOP, PROG, WPC)                                                            \
+  [&] {                                                                                            \
+    hipLaunchKernelGGL((k_probe<TB, C, HALF, IOP, PROG, WPC>), dim3(8u << (20 - TB), oct),         \
+                       dim3(1 << (TB - 4)), 0, 0, st, og, B, coefs, tabs);                         \
+  }
+  if (argc > 2 && argv[2][0] == 'p') {
+    // A13 after an idle gap / after a burner / back to back (argv[2] = "pre")
+    double* sink;
+    CHECK(hipMalloc(&sink, 8));
+    auto a13 = LNCH(13, 13, true, 4, 2, 2);
+    auto a12 = LNCH(12, 12, true, 4, 0, 3);
+    for (int us : {0, 500, 2000}) {
+      auto sl = [&] { hipLaunchKernelGGL(k_sleep, dim3(1), dim3(64), 0, 0, us); };
+      auto bu = [&] { hipLaunchKernelGGL(k_burn, dim3(2048), dim3(256), 0, 0, us, sink); };
+      char na[64], nb[64];
+      snprintf(na, sizeof na, "sleep %d us", us);
+      snprintf(nb, sizeof nb, "burn %d us", us);
+      if (pair(na, sl, "A13 half, 2 WG/CU", a13)) return 1;
+      if (pair(nb, bu, "A13 half, 2 WG/CU", a13)) return 1;
+      if (pair(na, sl, "A12 (kdk3<7>)", a12)) return 1;
+      if (pair(nb, bu, "A12 (kdk3<7>)", a12)) return 1;
+    }
+    return 0;
+  }
+  if (argc > 2) {
+    for (int rep = 0; rep < 2; ++rep) {
+      if (pair("A12 (kdk3<7>)", LNCH(12, 12, true, 4, 0, 3), "B12 (kdk<6>)", LNCH(12, 4, false, 8, 1, 2)))
+        return 1;
+      if (pair("A13 half, 2 WG/CU", LNCH(13, 13, true, 4, 2, 2), "B12c5 full, 2 WG/CU",
+               LNCH(12, 5, false, 8, 5, 2)))
+        return 1;
+      if (pair("A13 half, 2 WG/CU", LNCH(13, 13, true, 4, 2, 2), "A13 half, 2 WG/CU",
+               LNCH(13, 13, true, 4, 2, 2)))
+        return 1;
+      if (pair("B12c5 full, 2 WG/CU", LNCH(12, 5, false, 8, 5, 2), "B12c5 full, 2 WG/CU",
+               LNCH(12, 5, false, 8, 5, 2)))
+        return 1;
+    }
+    return 0;
+  }
 #define RUN(NAME, TB, C, HALF, IOP, PROG, WPC)                                                   \
   if (run(NAME, [&] {                                                                            \
         hipLaunchKernelGGL((k_probe<TB, C, HALF, IOP, PROG, WPC>), dim3(8u << (20 - TB), oct),   \
