@@ -136,7 +136,10 @@ struct RecScalar {
   __device__ __forceinline__ int i(int rec, int e) const { return (int)p[8 * rec + e]; }
 };
 
-template <int N, int KIND, int QM = 15, typename Rec>
+// FRAME (unitary RX / RY kicks of a Pauli-frame pass, dtc_kernels.hip
+// frame12_records): every kick runs the form-B butterfly with the frame-signed
+// coefficient of d[3], no variant branch
+template <int N, int KIND, int QM = 15, bool FRAME = false, typename Rec>
 __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, int rec0) {
   // Every site of an active nibble runs (inactive sites carry the identity):
   // no data-dependent branches, so no register shuffles at merge points; the
@@ -168,8 +171,20 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, 
       else if (q == 1) run(std::integral_constant<int, 1>{});
       else if (q == 2) run(std::integral_constant<int, 2>{});
       else run(std::integral_constant<int, 3>{});
+    } else if constexpr (FRAME) {
+      static_assert(KIND == kKindRX || KIND == kKindRY, "Pauli-frame kicks: the unitary families");
+      const double f = R.d(k, 3);
+      auto run = [&](auto qtag) { layer_f<KIND, 2, decltype(qtag)::value>(v, f); };
+      if (q == 0) run(std::integral_constant<int, 0>{});
+      else if (q == 1) run(std::integral_constant<int, 1>{});
+      else if (q == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
     } else {
       const double f = R.d(k, 0);
+#ifdef DTC_VAR_PROBE
+      // timing probe only (wrong results by design): one butterfly variant
+      auto run = [&](auto qtag) { layer_f<KIND, 2, decltype(qtag)::value>(v, f); };
+#else
       const int var = R.i(k, 1);
       auto run = [&](auto qtag) {
         constexpr int Q = decltype(qtag)::value;
@@ -178,6 +193,7 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, 
         else if (var == 2) layer_f<KIND, 2, Q>(v, f);
         else layer_f<KIND, 3, Q>(v, f);
       };
+#endif
       if (q == 0) run(std::integral_constant<int, 0>{});
       else if (q == 1) run(std::integral_constant<int, 1>{});
       else if (q == 2) run(std::integral_constant<int, 2>{});
@@ -189,14 +205,25 @@ __device__ __forceinline__ void apply_nibble(double2 (&v)[kRegs], const Rec& R, 
 // Tile re-layout through LDS.  No barrier before the writes: a thread writes
 // exactly the slots it read itself in the previous exchange (that one ended in
 // layout FROM), so no other thread can still need them.
+// xw, xr (Pauli-frame passes): the frame's X bits this re-layout flushes,
+// on the write side (thread bits of FROM) and the read side (thread bits of
+// TO): index y is written at slot(y ^ xw), read from slot(y ^ xr), so the
+// tile comes out X^(xw ^ xr)-permuted, and the register offsets stay
+// compile-time immediates.  A thread then no longer writes only slots it read
+// itself in the previous re-layout when xw or that one's xr is nonzero: the
+// caller passes sync for those.
 template <int FROM, int TO>
-__device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, int t) {
+__device__ __forceinline__ void exchange(double2 (&v)[kRegs], double2* s_tile, int t, int xw = 0,
+                                         int xr = 0, bool sync = false) {
   if (FROM == TO) return;
+  constexpr int kThrF = (kTile - 1) & ~(15 << (4 * FROM)), kThrT = (kTile - 1) & ~(15 << (4 * TO));
+  const int yw = ybase<FROM>(t) ^ (xw & kThrF), yr = ybase<TO>(t) ^ (xr & kThrT);
+  if (sync) __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(tile_y<FROM>(t, r))] = v[r];
+  for (int r = 0; r < kRegs; ++r) s_tile[lds_slot(yw | (r << (4 * FROM)))] = v[r];
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(tile_y<TO>(t, r))];
+  for (int r = 0; r < kRegs; ++r) v[r] = s_tile[lds_slot(yr | (r << (4 * TO)))];
 }
 
 // The same re-layout through a half-tile buffer, real parts then imaginary
@@ -223,13 +250,18 @@ __host__ __device__ constexpr int slot_add(int y) { return y ^ ((y >> 4) & 15) ^
 #define DTC_SLOT(base, LAY, r) ((base) ^ slot_add((r) << (4 * (LAY))))
 #endif
 template <int FROM, int TO>
-__device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t) {
+__device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_half, int t, int xw = 0,
+                                               int xr = 0) {
   if (FROM == TO) return;
   // the two per-thread bases are made opaque here, so every exchange forms
   // them afresh instead of the compiler keeping addresses live across the
   // kernel (the 12-site K-D-K at three workgroups per CU once spilled 80 B/lane
   // for 16 slot addresses per layout, r3h)
   int bf = slot_add(ybase<FROM>(t)), bt = slot_add(ybase<TO>(t));
+#ifndef DTC_ADD_SLOTS
+  bf ^= slot_add(xw);  // the frame's X flushes (exchange above)
+  bt ^= slot_add(xr);
+#endif
   asm volatile("" : "+v"(bf), "+v"(bt));
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) s_half[DTC_SLOT(bf, FROM, r)] = v[r].x;
@@ -247,42 +279,54 @@ __device__ __forceinline__ void exchange_split(double2 (&v)[kRegs], double* s_ha
 // Two tiles re-laid out together (the dual pass's forward and echo tiles),
 // each through its own half-tile buffer with the same slots: three barriers
 // for both.  Each buffer follows exchange_split's slot discipline.
+// (each tile with its own frame's flushes: vw, vr and ww, wr, exchange above)
 template <int FROM, int TO>
 __device__ __forceinline__ void exchange_split2(double2 (&v)[kRegs], double2 (&w)[kRegs],
-                                                double* s_a, double* s_b, int t) {
+                                                double* s_a, double* s_b, int t, int vw = 0,
+                                                int vr = 0, int ww = 0, int wr = 0) {
   if (FROM == TO) return;
   int bf = slot_add(ybase<FROM>(t)), bt = slot_add(ybase<TO>(t));
-  asm volatile("" : "+v"(bf), "+v"(bt));
+  int bw = bf, bu = bt;
+#ifndef DTC_ADD_SLOTS
+  bf ^= slot_add(vw);
+  bt ^= slot_add(vr);
+  bw ^= slot_add(ww);
+  bu ^= slot_add(wr);
+#endif
+  asm volatile("" : "+v"(bf), "+v"(bt), "+v"(bw), "+v"(bu));
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) {
     s_a[DTC_SLOT(bf, FROM, r)] = v[r].x;
-    s_b[DTC_SLOT(bf, FROM, r)] = w[r].x;
+    s_b[DTC_SLOT(bw, FROM, r)] = w[r].x;
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) {
     v[r].x = s_a[DTC_SLOT(bt, TO, r)];
-    w[r].x = s_b[DTC_SLOT(bt, TO, r)];
+    w[r].x = s_b[DTC_SLOT(bu, TO, r)];
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) {
     s_a[DTC_SLOT(bf, FROM, r)] = v[r].y;
-    s_b[DTC_SLOT(bf, FROM, r)] = w[r].y;
+    s_b[DTC_SLOT(bw, FROM, r)] = w[r].y;
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) {
     v[r].y = s_a[DTC_SLOT(bt, TO, r)];
-    w[r].y = s_b[DTC_SLOT(bt, TO, r)];
+    w[r].y = s_b[DTC_SLOT(bu, TO, r)];
   }
 }
 
+// (Pauli-frame masks: xw, xr, sync as exchange takes them; cw, cr the
+// cumulative ones exchange_split takes)
 template <bool SPLIT, int FROM, int TO>
 __device__ __forceinline__ void xch_tile(double2 (&v)[kRegs], double2* s_tile, double* s_half,
-                                         int t) {
-  if constexpr (SPLIT) exchange_split<FROM, TO>(v, s_half, t);
-  else exchange<FROM, TO>(v, s_tile, t);
+                                         int t, int xw = 0, int xr = 0, int cw = 0, int cr = 0,
+                                         bool sync = false) {
+  if constexpr (SPLIT) exchange_split<FROM, TO>(v, s_half, t, cw, cr);
+  else exchange<FROM, TO>(v, s_tile, t, xw, xr, sync);
 }
 
 __device__ __forceinline__ double2 diag_phase(const double2* s_chunk, int n_chunks, int64_t x) {

@@ -182,6 +182,14 @@ static constexpr int kRecTotal = 2 * kTileBits;
 // the X masks the four re-layouts flush (tile bits) and the Z mask of the
 // diagonal
 enum : int { kT13MaskX1 = 3, kT13MaskX2 = 4, kT13MaskX3 = 5, kT13MaskX4 = 6, kT13MaskZ = 7 };
+// 12-bit passes of the unitary RX / RY families (frame12_records, pass_body
+// with FR): every kick record also holds the frame-signed form-B coefficient
+// in d[3] (d[0], i[1] keep the variant form for the passes that measure X in
+// flight), the total record the X masks of the pass's real re-layouts in
+// program order (i[3 ..]: write side in bits 0..11, read side in 16..27) and
+// the diagonal's Z mask with the frame's extra power of i in bits 16, 17 (i[7])
+static constexpr int kFrameCoef = 3;
+enum : int { kT12MaskX0 = 3, kT12MaskZ = 7, kT12PhShift = 16 };
 
 // One pass's kick layers, as the prep kernel needs them.
 struct PassKick {

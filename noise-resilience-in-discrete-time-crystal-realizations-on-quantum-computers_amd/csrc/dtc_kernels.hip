@@ -301,12 +301,107 @@ __device__ int frame13_records(const PassKick& pk, KickRec* out, const int* fvar
     kick(1, 8);
     for (int q = 4; q <= 7; ++q) kick(1, q);
   }
+  // cumulative: the X flushed by re-layouts 1 .. e (the kernel's xch)
   tot.i[kT13MaskX1] = m1;
-  tot.i[kT13MaskX2] = m2;
-  tot.i[kT13MaskX3] = m3;
-  tot.i[kT13MaskX4] = m4;
+  tot.i[kT13MaskX2] = m1 ^ m2;
+  tot.i[kT13MaskX3] = m1 ^ m2 ^ m3;
+  tot.i[kT13MaskX4] = m1 ^ m2 ^ m3 ^ m4;
   tot.i[kT13MaskZ] = md;
   return ph;
+}
+
+// The same Pauli-frame records for the 12-bit K-D-K passes of the unitary
+// families (pass_body FR: nibble sets 6 and 7, the standard geometry).  Their
+// program (RoundPlan): pre-kick nibbles IO -> 0 -> O with a re-layout before
+// each but the first, the diagonal, post-kick nibbles O -> 0 -> IO, re-layouts
+// skipped where a layout does not change.  A kick's X is flushed by the first
+// re-layout after it within its half, else (the half's last nibble) by the
+// last one before it; the diagonal flushes Z as in frame13_records (for a
+// pass without one, the global factor's multiply; for a dual pass's echo
+// branch, copied before the diagonal, its own sign flush).  The coefficients
+// go to d[kFrameCoef], the masks and the extra power of i to tot (kT12*).
+__device__ void frame12_records(const PassKick& pk, KickRec* out, const int* fvar, KickRec& tot) {
+  constexpr int NT = kTileBits;
+  const bool rx = pk.kind == kKindRX;
+  int nibs = 0;
+  for (int n = 0; n < 3; ++n)
+    if (pk.act & (0xF << (4 * n))) nibs |= 1 << n;
+  const bool pre = pk.pre.enabled, post = pk.post.enabled;
+  const int IO = io_layout(nibs), O = 3 - IO;
+  const bool n0 = nibs & 1, nIO = (nibs >> IO) & 1, nO = (nibs >> O) & 1;
+  const int d_lay = pre ? (nO ? O : (n0 ? 0 : IO)) : IO;
+  const int pO = nO ? O : d_lay, p0 = n0 ? 0 : pO, pIO = nIO ? IO : p0;
+  // the program: nibble kicks (h * 4 + nibble), re-layouts (-1), the diagonal (-2)
+  int ev[12], ne = 0;
+  if (pre) {
+    if (nIO) ev[ne++] = IO;
+    if (n0) { ev[ne++] = -1; ev[ne++] = 0; }
+    if (nO) { ev[ne++] = -1; ev[ne++] = O; }
+  }
+  ev[ne++] = -2;
+  if (post) {
+    if (nO) { if (d_lay != O) ev[ne++] = -1; ev[ne++] = 4 + O; }
+    if (n0) { if (pO != 0) ev[ne++] = -1; ev[ne++] = 4 + 0; }
+    if (nIO) { if (p0 != IO) ev[ne++] = -1; ev[ne++] = 4 + IO; }
+    if (pIO != IO) ev[ne++] = -1;
+  } else if (d_lay != IO) {
+    ev[ne++] = -1;
+  }
+  auto form_a = [&](int i) { return (fvar[i] >> 1) ^ 1; };
+  auto zbit = [&](int i) { return rx ? (fvar[i] & 1) : ((fvar[i] & 1) ^ form_a(i)); };
+  // each kicked nibble's flush: the re-layout it is assigned to, on the read
+  // side when the re-layout follows the kick (the sites are register bits of
+  // its source layout, thread bits of its target: mr), on the write side when
+  // it precedes it (register bits of the target, thread bits of the source:
+  // mw) -- either way the mask stays off the side's register offsets
+  int mw[4] = {0, 0, 0, 0}, mr[4] = {0, 0, 0, 0};
+  {
+    int xi = 0;  // re-layouts seen so far
+    for (int e = 0; e < ne; ++e) {
+      if (ev[e] == -1) ++xi;
+      if (ev[e] < 0) continue;
+      const int h = ev[e] >> 2, nib = ev[e] & 3;
+      // the first re-layout after it within its half, else the last before it
+      int after = -1, k = xi;
+      for (int f = e + 1; f < ne && ev[f] != -2; ++f)
+        if (ev[f] == -1) { after = k; break; }
+      int m = 0;
+      for (int q = 0; q < 4; ++q) m |= form_a(h * NT + 4 * nib + q) << (4 * nib + q);
+      if (after >= 0 && after < 4) mr[after] |= m;
+      else if (after < 0 && xi >= 1 && xi <= 4) mw[xi - 1] |= m;
+    }
+  }
+  int npost = 0;
+  if (post)
+    for (int k = 0; k < NT; ++k)
+      if ((nibs >> (k >> 2)) & 1) npost |= zbit(NT + k) << k;
+  int x = 0, z = 0, ph = 0, xi = 0, md = 0;
+  for (int e = 0; e < ne; ++e) {
+    if (ev[e] == -1) {
+      const int m = xi < 4 ? mw[xi] ^ mr[xi] : 0;
+      ph += 2 * (__popc(z & m) & 1);
+      x ^= m;
+      ++xi;
+    } else if (ev[e] == -2) {
+      md = z ^ npost;
+      z ^= md;
+    } else {
+      const int h = ev[e] >> 2, nib = ev[e] & 3;
+      for (int q = 0; q < 4; ++q) {
+        const int k = 4 * nib + q, i = h * NT + k;
+        const int fa = form_a(i), n2 = zbit(i);
+        const double g = fa ? -out[i].d[0] : out[i].d[0];
+        const int flip = ((rx ? z : (x ^ z)) >> k) & 1;
+        out[i].d[kFrameCoef] = flip ? -g : g;
+        ph += (rx ? 3 * fa : 2 * fa) + 2 * flip;
+        x ^= fa << k;
+        ph += 2 * (n2 & (x >> k) & 1);
+        z ^= n2 << k;
+      }
+    }
+  }
+  for (int e = 0; e < 4; ++e) tot.i[kT12MaskX0 + e] = mw[e] | (mr[e] << 16);
+  tot.i[kT12MaskZ] = md | ((ph & 3) << kT12PhShift);
 }
 
 // Kick records (dtc_kernels.h: KickRec) of n_pass passes x batch states: one
@@ -438,6 +533,10 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   double w[2] = {1.0, 1.0};
   const int tb = pk.tb == kMaxTileBits ? kMaxTileBits : kTileBits;
   const bool frame13 = tb == kMaxTileBits && (pk.kind == kKindRX || pk.kind == kKindRY);
+  // (the 12-bit passes' frame records, pass_body FR: nibble sets 6 and 7 of
+  // the standard geometry -- not the 13 / 7 split's 7-site column group)
+  const bool frame12 = tb == kTileBits && (pk.kind == kKindRX || pk.kind == kKindRY) &&
+                       (pk.act & 0xF0) && (pk.act & 0xF00) && !(pk.c == kB7Cols && pk.act == 0xFE0);
   int fvar[2 * kMaxTileBits];
   for (int half = 0; half < 2; ++half) {
     const KickDesc& K = half == 0 ? pk.pre : pk.post;
@@ -472,7 +571,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
         for (int e = 3; e < 8; ++e) r.d[e] = 0.0;
       }
       out[half * tb + k] = r;
-      if (frame13) fvar[half * tb + k] = sm.var;
+      if (frame13 || frame12) fvar[half * tb + k] = sm.var;
       ksum += sm.k;
       w[half] *= sm.scale;
     }
@@ -480,6 +579,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs P) {
   KickRec tot;
   for (int e = 0; e < 8; ++e) tot.d[e] = 0.0;
   if (frame13) ksum += frame13_records(pk, out, fvar, tot);
+  if (frame12) frame12_records(pk, out, fvar, tot);
   const int kph = ksum & 3;
   const double wg = w[0] * w[1];
   tot.d[0] = kph == 0 ? wg : (kph == 2 ? -wg : 0.0);
@@ -515,6 +615,18 @@ struct RoundPlan {
   static constexpr int pO = nO ? O : d_lay;
   static constexpr int p0 = n0 ? 0 : pO;
   static constexpr int pIO = nIO ? IO : p0;
+  // Pauli-frame passes: the real re-layouts in program order (their X-flush
+  // masks; frame12_records walks the same sequence): pre IO -> 0 (xA), pre ->
+  // O (xB); post d_lay -> O (x1), -> 0 (x2), -> IO (x3), -> IO (x4); without
+  // a post-kick d_lay -> IO (x5)
+  static constexpr int xA = 0;
+  static constexpr int xB = (pre && n0) ? 1 : 0;
+  static constexpr int npre = (pre && n0 ? 1 : 0) + (pre && nO ? 1 : 0);
+  static constexpr bool r1 = post && nO && d_lay != O;
+  static constexpr bool r2 = post && n0 && pO != 0;
+  static constexpr bool r3 = post && nIO && p0 != IO;
+  static constexpr int x1 = npre, x2 = x1 + (r1 ? 1 : 0), x3 = x2 + (r2 ? 1 : 0),
+                       x4 = x3 + (r3 ? 1 : 0), x5 = npre;
 };
 
 // Development-only phase timing (build with -DDTC_PHASE_TIMING): wave 0 of
@@ -705,6 +817,65 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // flight.  Explicit, so no use of them waits for the tile.
   static_assert(kRegs == 16, "vmcnt immediate assumes 16 tile loads");
   __builtin_amdgcn_s_waitcnt(0x4F70);
+  // Pauli-frame kicks (frame12_records): the unitary families' passes over
+  // nibble sets 6 and 7 that measure no X in flight run one butterfly per
+  // kick; the frame's X bits leave through the re-layouts' write slots
+  // (fxm: mask of re-layout e in program order, RoundPlan::x*), its Z bits
+  // through the diagonal (fzm: a sign per amplitude, in the window table and
+  // the thread's phase) and its extra power of i through the global factor
+#ifdef DTC_ADD_SLOTS
+  constexpr bool FR = false;  // (the additive slots are not linear over XOR)
+#else
+  // (the 8-site column group's plain passes keep the variant branches: with
+  // frames their full-tile re-layouts take the flush barriers and ran 1-2 %
+  // slower, r6v / r6w; its dual passes, the 12-site group's and every final
+  // pass gain -- dual<7> 9.60 -> 8.62 ms, kdk_final<7> 6.0 -> 5.3, C2 +1.5 %)
+#ifdef DTC_FR_ALL_NIBS  // development A/B: frames for the 8-site group's plain passes too
+  constexpr bool FR = (KIND == kKindRX || KIND == kKindRY) && MC != 3 && (NIBS == 6 || NIBS == 7) &&
+                      GEO == kGeoStd;
+#else
+  constexpr bool FR = (KIND == kKindRX || KIND == kKindRY) && MC != 3 &&
+                      (NIBS == 7 || (NIBS == 6 && DUAL)) && GEO == kGeoStd;
+#endif
+#endif
+  const int fzw = FR ? R.i(kRecTotal, kT12MaskZ) : 0;
+  const int fzm = fzw & (kTile - 1);
+  // re-layout e's write-side and read-side masks, and the cumulative ones of
+  // re-layouts 0 .. e (the XOR-slot re-layouts, dtc_device.h exchange_split)
+  auto fxw = [&](int e) { return (FR && e >= 0) ? (int)(R.i(kRecTotal, kT12MaskX0 + e) & 0xFFFF) : 0; };
+  auto fxr = [&](int e) {
+    return (FR && e >= 0) ? (int)((R.i(kRecTotal, kT12MaskX0 + e) >> 16) & 0xFFFF) : 0;
+  };
+  auto fxm = [&](int e) {
+    int c = 0;
+    for (int k = 0; k <= e; ++k) c ^= fxw(k) ^ fxr(k);
+    return c;
+  };
+  // re-layout e of the forward tile (RoundPlan::x*)
+  auto xch_f = [&](auto from_tag, auto to_tag, int e) {
+    constexpr int F = decltype(from_tag)::value, T = decltype(to_tag)::value;
+    // (the pass's first re-layout has no earlier reads to wait for)
+    xch_tile<SPLIT, F, T>(v, s_tile, s_half, t, fxw(e), fxr(e), fxm(e - 1), fxm(e),
+                          e > 0 && (fxw(e) | fxr(e - 1)) != 0);
+  };
+  // i^k g
+  auto rot_i = [](double2 g, int k) {
+    return k == 0 ? g : (k == 1 ? make_double2(-g.y, g.x) : (k == 2 ? make_double2(-g.x, -g.y)
+                                                                     : make_double2(g.y, -g.x)));
+  };
+  // a Z flush without a diagonal to carry it: amplitude y of layout LAY
+  // negated when popcount(y & zm) is odd (sign-bit XORs, no branch)
+  auto zflush = [&](auto lay_tag, double2 (&x)[kRegs], int zm) {
+    constexpr int LAY = decltype(lay_tag)::value;
+    const uint32_t mt = (__popc(ybase<LAY>(t) & zm) & 1) ? 0x80000000u : 0u;
+    const int zr = (zm >> (4 * LAY)) & 15;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+      const uint64_t m = (uint64_t)(mt ^ ((__popc(r & zr) & 1) ? 0x80000000u : 0u)) << 32;
+      x[r].x = __longlong_as_double(__double_as_longlong(x[r].x) ^ m);
+      x[r].y = __longlong_as_double(__double_as_longlong(x[r].y) ^ m);
+    }
+  };
   if (RP::diag) {
     const double cs = A.diag_conj ? -1.0 : 1.0;
 #pragma unroll
@@ -712,7 +883,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       const int i = t + j * kThreads;
       if (i < A.n_chunks * 64) s_chunk[i] = make_double2(dchunk[j].x, cs * dchunk[j].y);
     }
-    if (g0 >= 0 && t < 64) s_win[t] = make_double2(dwin.x, cs * dwin.y);
+    // (FR: the window entry of register bits (t >> 1) & 15 of layout d_lay
+    // takes their share of the frame's Z flush)
+    const double zs = (FR && (__popc((t >> 1) & (fzm >> (4 * RP::d_lay)) & 15) & 1)) ? -1.0 : 1.0;
+    if (g0 >= 0 && t < 64) s_win[t] = make_double2(zs * dwin.x, zs * cs * dwin.y);
     if (kSplitDiag && t < 64) s_win2[t] = make_double2(dwin2.x, cs * dwin2.y);
     // made visible by the first exchange's barrier, or by this one
     if constexpr (!(RP::pre && (RP::n0 || RP::nO))) __syncthreads();
@@ -722,7 +896,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // the diagonal (the state's arithmetic does not depend on whether it is
   // measured; a measurement between the diagonal and the post-kick divides
   // its sums by w_post^2)
-  const double2 gph = make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1));
+  const double2 gph = rot_i(make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1)),
+                            (fzw >> kT12PhShift) & 3);
   const double inv_w2_mid = R.d(kRecTotal, 2);
 
   auto diag_in = [&](auto lay_tag, bool with_g) {
@@ -750,8 +925,10 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     // nibble of layout LAY inside or outside the column bits: g0 >= 0)
     const int w0i = (int)(((x0 << 1) >> g0) & 63);
     const double2 w0 = s_win[w0i];
-    const double2 pc = cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)),
-                            with_g ? gph : make_double2(1.0, 0.0));
+    const double2 pc0 = cmul(cmul(diag_phase(s_chunk, A.n_chunks, x0), make_double2(w0.x, -w0.y)),
+                             with_g ? gph : make_double2(1.0, 0.0));
+    // (FR: the thread bits' share of the frame's Z flush)
+    const double2 pc = (FR && (__popc(ybase<LAY>(t) & fzm) & 1)) ? make_double2(-pc0.x, -pc0.y) : pc0;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], cmul(pc, s_win[w0i | (r << 1)]));
   };
@@ -1045,19 +1222,19 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     double sc = 1.0;
     if constexpr (RP::nIO) {
       if (x_pre) measure_x_pre(LIO{}, sc);
-      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, 0);
+      apply_nibble<RP::IO, KIND, qm(RP::IO), FR>(v, R, 0);
       if (x_pre) sc *= nib_w2(RP::IO, 0);
     }
     if constexpr (RP::n0) {
-      xch_tile<SPLIT, RP::IO, 0>(v, s_tile, s_half, t);
+      xch_f(LIO{}, L0{}, RP::xA);
       if (x_pre) measure_x_pre(L0{}, sc);
-      apply_nibble<0, KIND, qm(0)>(v, R, 0);
+      apply_nibble<0, KIND, qm(0), FR>(v, R, 0);
       if (x_pre) sc *= nib_w2(0, 0);
     }
     if constexpr (RP::nO) {
-      xch_tile<SPLIT, RP::n0 ? 0 : RP::IO, RP::O>(v, s_tile, s_half, t);
+      xch_f(std::integral_constant<int, RP::n0 ? 0 : RP::IO>{}, LO{}, RP::xB);
       if (x_pre) measure_x_pre(LO{}, sc);
-      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, 0);
+      apply_nibble<RP::O, KIND, qm(RP::O), FR>(v, R, 0);
     }
   }
   DTC_TS(3);
@@ -1072,10 +1249,23 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // before the stores.
   constexpr bool kCo = DUAL && RP::post;
   double2 w[DUAL ? kRegs : 1];
+  // the echo branch's frame (its records R2): Z flushed here, where the branch
+  // leaves the forward before the diagonal; X masks at the shared re-layouts
+  const int fzw2 = (FR && kCo) ? R2.i(kRecTotal, kT12MaskZ) : 0;
+  auto fxm2 = [&](int e) {  // cumulative, as fxm
+    int c = 0;
+    if (FR && kCo)
+      for (int k = 0; k <= e; ++k) {
+        const int m = (int)R2.i(kRecTotal, kT12MaskX0 + k);
+        c ^= (m & 0xFFFF) ^ ((m >> 16) & 0xFFFF);
+      }
+    return c;
+  };
   if constexpr (kCo) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
     if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
+    if constexpr (FR) zflush(std::integral_constant<int, RP::d_lay>{}, w, fzw2 & (kTile - 1));
   } else if constexpr (DUAL) {
     // the echo branch: E = K'_1 K_p (input) -- the forward pass's D, its
     // post-kick K_{p+1} and the echo's D^* and undo of K_{p+1} cancel exactly
@@ -1117,6 +1307,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     // post-kick, so applying it here, before any measurement, is exact)
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) v[r] = cmul(v[r], gph);
+    if constexpr (FR) zflush(std::integral_constant<int, RP::d_lay>{}, v, fzm);
   }
   // ---- diagonal and measurement at d_lay ----
   using DL = std::integral_constant<int, RP::d_lay>;
@@ -1133,21 +1324,25 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (kCo) {
     static_assert(SPLIT, "co-traversed dual pass: half-tile re-layouts");
     if constexpr (RP::nO) {
-      exchange_split2<RP::d_lay, RP::O>(v, w, s_half, s_half2, t);
-      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, kTileBits);
-      apply_nibble<RP::O, KIND, qm(RP::O)>(w, R2, kTileBits);
+      exchange_split2<RP::d_lay, RP::O>(v, w, s_half, s_half2, t, fxm(RP::x1 - 1), fxm(RP::x1),
+                                     fxm2(RP::x1 - 1), fxm2(RP::x1));
+      apply_nibble<RP::O, KIND, qm(RP::O), FR>(v, R, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O), FR>(w, R2, kTileBits);
     }
     if constexpr (RP::n0) {
-      exchange_split2<RP::pO, 0>(v, w, s_half, s_half2, t);
-      apply_nibble<0, KIND, qm(0)>(v, R, kTileBits);
-      apply_nibble<0, KIND, qm(0)>(w, R2, kTileBits);
+      exchange_split2<RP::pO, 0>(v, w, s_half, s_half2, t, fxm(RP::x2 - 1), fxm(RP::x2),
+                                     fxm2(RP::x2 - 1), fxm2(RP::x2));
+      apply_nibble<0, KIND, qm(0), FR>(v, R, kTileBits);
+      apply_nibble<0, KIND, qm(0), FR>(w, R2, kTileBits);
     }
     if constexpr (RP::nIO) {
-      exchange_split2<RP::p0, RP::IO>(v, w, s_half, s_half2, t);
-      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, kTileBits);
-      apply_nibble<RP::IO, KIND, qm(RP::IO)>(w, R2, kTileBits);
+      exchange_split2<RP::p0, RP::IO>(v, w, s_half, s_half2, t, fxm(RP::x3 - 1), fxm(RP::x3),
+                                     fxm2(RP::x3 - 1), fxm2(RP::x3));
+      apply_nibble<RP::IO, KIND, qm(RP::IO), FR>(v, R, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO), FR>(w, R2, kTileBits);
     }
-    exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t);
+    exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t, fxm(RP::x4 - 1), fxm(RP::x4),
+                                     fxm2(RP::x4 - 1), fxm2(RP::x4));
     if constexpr (kRho) {
       rho_apply(LIO{}, kTileBits, v, R);
       rho_apply(LIO{}, kTileBits, w, R2);
@@ -1155,26 +1350,26 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   } else if constexpr (RP::post) {
     double sc = inv_w2_mid;
     if constexpr (RP::nO) {
-      xch_tile<SPLIT, RP::d_lay, RP::O>(v, s_tile, s_half, t);
+      xch_f(std::integral_constant<int, RP::d_lay>{}, std::integral_constant<int, RP::O>{}, RP::x1);
       if (x_post) measure_x_post(LO{}, sc);
-      apply_nibble<RP::O, KIND, qm(RP::O)>(v, R, kTileBits);
+      apply_nibble<RP::O, KIND, qm(RP::O), FR>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(RP::O, kTileBits);
     }
     if constexpr (RP::n0) {
-      xch_tile<SPLIT, RP::pO, 0>(v, s_tile, s_half, t);
+      xch_f(std::integral_constant<int, RP::pO>{}, std::integral_constant<int, 0>{}, RP::x2);
       if (x_post) measure_x_post(L0{}, sc);
-      apply_nibble<0, KIND, qm(0)>(v, R, kTileBits);
+      apply_nibble<0, KIND, qm(0), FR>(v, R, kTileBits);
       if (x_post) sc *= nib_w2(0, kTileBits);
     }
     if constexpr (RP::nIO) {
-      xch_tile<SPLIT, RP::p0, RP::IO>(v, s_tile, s_half, t);
+      xch_f(std::integral_constant<int, RP::p0>{}, std::integral_constant<int, RP::IO>{}, RP::x3);
       if (x_post) measure_x_post(LIO{}, sc);
-      apply_nibble<RP::IO, KIND, qm(RP::IO)>(v, R, kTileBits);
+      apply_nibble<RP::IO, KIND, qm(RP::IO), FR>(v, R, kTileBits);
     }
-    xch_tile<SPLIT, RP::pIO, RP::IO>(v, s_tile, s_half, t);
+    xch_f(std::integral_constant<int, RP::pIO>{}, std::integral_constant<int, RP::IO>{}, RP::x4);
     if constexpr (kRho) rho_apply(LIO{}, kTileBits, v, R);
   } else {
-    xch_tile<SPLIT, RP::d_lay, RP::IO>(v, s_tile, s_half, t);
+    xch_f(std::integral_constant<int, RP::d_lay>{}, std::integral_constant<int, RP::IO>{}, RP::x5);
   }
   if constexpr (MC > 0) {
     if (A.meas != kMeasNone && A.meas_at_end) measure_in(LIO{}, 1.0);
@@ -1210,7 +1405,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (kCo) {
     // the echo branch's tile, after the forward's: its global factor i^k w
     // of K_p and of K'_1
-    const double2 gE = make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1));
+    const double2 gE = rot_i(make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1)),
+                             (fzw2 >> kT12PhShift) & 3);
     char* d2 = (char*)(A.dst2 + sbase);
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {

@@ -72,20 +72,16 @@ __device__ __forceinline__ int ythr(int t) {
 // 1) << 4, made L0's writes two-way: 256 conflict cycles per wave, r6e).
 __host__ __device__ constexpr int slot(int y) { return y ^ ((y >> 4) & 31); }
 
-template <int FROM, int TO, bool FIRST = false>
-__device__ __forceinline__ void xch(double2 (&v)[kRegs], double* s_half, int t, int xm = 0) {
-  // xm: the Pauli frame's X bits this re-layout flushes (frame13_records): the
-  // writes go to slot(y ^ xm) = slot(y) ^ slot(xm), so the tile comes out
-  // X^xm-permuted
-  int bf = slot(ythr<FROM>(t)) ^ slot(xm), bt = slot(ythr<TO>(t));
+template <int FROM, int TO>
+__device__ __forceinline__ void xch(double2 (&v)[kRegs], double* s_half, int t, int xw = 0, int xr = 0) {
+  // xw, xr: the Pauli frame's X bits flushed by the pass's re-layouts before
+  // and including this one (frame13_records, cumulative): index y is written
+  // at slot(y ^ xw), read from slot(y ^ xr) (slot is linear over XOR), so the
+  // tile comes out X^(xw ^ xr)-permuted and no barrier precedes the writes: a
+  // thread writes exactly the slots it read itself in the previous re-layout
+  // (which ended in layout FROM, read with this one's xw)
+  int bf = slot(ythr<FROM>(t)) ^ slot(xw), bt = slot(ythr<TO>(t)) ^ slot(xr);
   asm volatile("" : "+v"(bf), "+v"(bt));
-  // no barrier before the writes when xm = 0: a thread writes exactly the
-  // slots it read itself in the previous re-layout (which ended in layout
-  // FROM); a flush writes other threads' slots, so it waits for their reads
-  // (FIRST: the pass's first re-layout, no reads before it)
-#ifndef DTC_T13_NOBAR_PROBE  // timing probe only (wrong results by design)
-  if (!FIRST && xm) __syncthreads();
-#endif
 #pragma unroll
   for (int r = 0; r < kRegs; ++r) s_half[bf ^ slot(yreg(FROM, r))] = v[r].x;
   __syncthreads();
@@ -235,12 +231,12 @@ __device__ __forceinline__ void pass13_body(const PassArgs& A) {
     kick4<LIO, KIND>(v, R, 0);
     swap_reg_lane<0, 16>(v);
     kick<0, KIND>(v, R, 8);
-    xch<LIOs, L0, true>(v, s_half, t, R.i(kRecTot, kT13MaskX1));
+    xch<LIOs, L0>(v, s_half, t, 0, R.i(kRecTot, kT13MaskX1));
     kick4<L0, KIND>(v, R, 0);
-    xch<L0, L9>(v, s_half, t, R.i(kRecTot, kT13MaskX2));
+    xch<L0, L9>(v, s_half, t, R.i(kRecTot, kT13MaskX1), R.i(kRecTot, kT13MaskX2));
     kick4<L9, KIND>(v, R, 0);
   } else if constexpr (DIAG) {
-    xch<LIO, L9, true>(v, s_half, t);
+    xch<LIO, L9>(v, s_half, t);
   }
   if constexpr (!DIAG) {
     // the global factor and the Z flush (L9: register bits = tile bits 9..12)
@@ -278,14 +274,15 @@ __device__ __forceinline__ void pass13_body(const PassArgs& A) {
   // ---- post-kick: L9 9..12, L0 0..3, (LIOs) 8, swap back, LIO 4..7 ----
   if constexpr (POST) {
     kick4<L9, KIND>(v, R, kBits);
-    xch<L9, L0>(v, s_half, t, R.i(kRecTot, kT13MaskX3));
+    xch<L9, L0>(v, s_half, t, R.i(kRecTot, kT13MaskX2), R.i(kRecTot, kT13MaskX3));
     kick4<L0, KIND>(v, R, kBits);
-    xch<L0, LIOs>(v, s_half, t, R.i(kRecTot, kT13MaskX4));
+    xch<L0, LIOs>(v, s_half, t, R.i(kRecTot, kT13MaskX3), R.i(kRecTot, kT13MaskX4));
     kick<0, KIND>(v, R, kBits + 8);
     swap_reg_lane<0, 16>(v);
     kick4<LIO, KIND>(v, R, kBits);
   } else if constexpr (PRE || DIAG) {
-    xch<L9, LIO>(v, s_half, t);
+    // (no flush of its own: the slot map the pre-kick's re-layouts left)
+    xch<L9, LIO>(v, s_half, t, R.i(kRecTot, kT13MaskX2), R.i(kRecTot, kT13MaskX2));
   }
   if constexpr (MC == 1) {
     if (A.meas != kMeasNone && A.meas_at_end) measure(CLIO{}, 1.0);
