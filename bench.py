@@ -362,10 +362,11 @@ def main(argv=None):
     ap.add_argument("--tf", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-traj", type=int, default=0,
-                    help="0 = six per host thread (c2: about 11 s on the GPU box's 16 cores)")
-    ap.add_argument("--cpu-tf", type=int, default=20,
-                    help="time points of the CPU sample (c2: about 10 s at four trajectories "
-                         "per host thread)")
+                    help="0 = three per host thread at c2 (about 12 s on the GPU box's 16 "
+                         "cores at T=30)")
+    ap.add_argument("--cpu-tf", type=int, default=0,
+                    help="time points of the CPU sample; 0 = the line's own tf (c2: T=30, "
+                         "the headline config; ctrl: 20; energy: 6)")
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "energy", "ctrl"), default="c2",
                     help="c2: BASELINE configs[1] (default, the headline line); c3: L=20 "
                          "device-like noise (stand-in calibration, data/"
@@ -506,7 +507,7 @@ def main(argv=None):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
         threads = host_cpu_info()["usable_cores"]
-        cpu = cpu_baseline(spec, args.cpu_traj or 6 * threads, args.cpu_tf, threads)
+        cpu = cpu_baseline(spec, args.cpu_traj or 3 * threads, args.cpu_tf or spec.T, threads)
 
     info = eng.device_info()
     c5 = None
@@ -1039,7 +1040,7 @@ def main_energy(args):
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_energy(spec, args.cpu_traj or 2 * _host_threads(),
-                                  min(args.cpu_tf, 6), _host_threads())
+                                  min(args.cpu_tf or 6, 6), _host_threads())
     res = {
         "metric": "Floquet-periods×trajectories/sec at L=20 with <Z_i>,<Z_iZ_i+1>,<X_i> per "
                   "period (energy path); RZZ-kernel HBM GB/s vs peak",
@@ -1120,9 +1121,9 @@ def main_ctrl(args):
     # (the optimisation loop's evaluation count is data-dependent: no fixed CPU work unit)
     if world == 1 and not args.no_cpu_baseline and not args.ctrl_opt:
         hs_, phis_ = load_disorder_row(L)
-        s = pkg.SweepSpec(L=L, T=args.cpu_tf, hs=hs_, phis=phis_, g=0.84, noise_prob=0.05,
+        s = pkg.SweepSpec(L=L, T=args.cpu_tf or 20, hs=hs_, phis=phis_, g=0.84, noise_prob=0.05,
                           use_noise=1, t_offset=1)
-        cpu = cpu_baseline(s, args.cpu_traj or 2 * _host_threads(), args.cpu_tf,
+        cpu = cpu_baseline(s, args.cpu_traj or 2 * _host_threads(), s.T,
                            _host_threads(), t_offset=1)
         cpu["unit"] = "periods*trajectories/s"
     if args.ctrl_opt:

@@ -13,8 +13,8 @@
 // dtc_lcw2_final: workgroups per CU (its 38.7 KB of LDS allow four; four cap
 // the kernel at 128 VGPRs, three at 168)
 #ifndef DTC_LCW3_WPS
-#ifdef DTC_LCW3_ADD
-#define DTC_LCW3_WPS 3  // 41.2 KB of LDS with the padded additive slots
+#if defined(DTC_LCW3_ADD) || defined(DTC_LCW3_MERGE)
+#define DTC_LCW3_WPS 3  // 41.2 KB of LDS with the padded additive slots, 49.7 with whole tables
 #else
 #define DTC_LCW3_WPS 4
 #endif
@@ -920,19 +920,28 @@ __device__ __forceinline__ int slot_base(int t) {
   return b;
 }
 // cone tables in LDS (double2 entries), natural index order from bit lo
-enum : int { kT6a = 0, kT6b, kT5a, kT5b, kT4a, kT4b, kT3a, kT3b, kT2, kT1, kNTab };
+// kT4 / kT3: the r = 4 and r = 3 diagonals whole (9 and 7 bits), formed in
+// LDS from their staged halves (T4[y] = T4a[y & 31] T4b[y >> 4], the halves
+// overlapping at j): one lookup and product per amplitude instead of two
+enum : int { kT6a = 0, kT6b, kT5a, kT5b, kT4a, kT4b, kT3a, kT3b, kT2, kT1, kT4, kT3, kNTab };
 __host__ __device__ constexpr int tab_off(int k) {
   return k == kT6a ? 0 : k == kT6b ? 64 : k == kT5a ? 192 : k == kT5b ? 256 : k == kT4a ? 320
-       : k == kT4b ? 352 : k == kT3a ? 384 : k == kT3b ? 400 : k == kT2 ? 416 : 448;
+       : k == kT4b ? 352 : k == kT3a ? 384 : k == kT3b ? 400 : k == kT2 ? 416 : k == kT1 ? 448
+       : k == kT4 ? 456 : 968;
 }
+static constexpr int kTabStaged = 456;  // entries staged from the instance's tables
+#ifdef DTC_LCW3_MERGE
+static constexpr int kTabEntries = 1096;
+#else
 static constexpr int kTabEntries = 456;
+#endif
 __host__ __device__ constexpr int tab_bits(int k) {
   return k == kT6a ? 6 : k == kT6b ? 7 : (k == kT5a || k == kT5b) ? 6 : (k == kT4a || k == kT4b) ? 5
-       : (k == kT3a || k == kT3b) ? 4 : k == kT2 ? 5 : 3;
+       : (k == kT3a || k == kT3b) ? 4 : k == kT2 ? 5 : k == kT1 ? 3 : k == kT4 ? 9 : 7;
 }
 __host__ __device__ constexpr int tab_lo(int k) {  // offset from j of index bit 0
-  return k == kT6a ? -5 : k == kT5a ? -5 : k == kT4a ? -4 : k == kT3a ? -3 : k == kT2 ? -2
-       : k == kT1 ? -1 : 0;
+  return k == kT6a ? -5 : k == kT5a ? -5 : (k == kT4a || k == kT4) ? -4 : (k == kT3a || k == kT3) ? -3
+       : k == kT2 ? -2 : k == kT1 ? -1 : 0;
 }
 __host__ __device__ constexpr int tab_layer(int k) {
   return (k == kT6a || k == kT6b) ? 0 : (k == kT5a || k == kT5b) ? 1 : (k == kT4a || k == kT4b) ? 2
@@ -1091,7 +1100,7 @@ __global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArg
   static_assert(tab_off(kT6b) == 64 && tab_off(kT5a) == 192 && tab_off(kT5b) == 256 &&
                     tab_off(kT4a) == 320 && tab_off(kT4b) == 352 && tab_off(kT3a) == 384 &&
                     tab_off(kT3b) == 400 && tab_off(kT2) == 416 && tab_off(kT1) == 448 &&
-                    kTabEntries == 456 && kThreads == 256,
+                    kTabStaged == 456 && kThreads == 256,
                 "the per-wave table split below");
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
   int s0, d0, s1 = -1, d1 = 0;
@@ -1141,6 +1150,16 @@ __global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArg
   kick(C3{}, C1{}, LCW3_S(p2));
   swap_reg_lane<0, 32>(v);  // register bit 0: m5 (lane bit 5: p3)
   kick(C0{}, C1{}, LCW3_S(m5));
+#ifdef DTC_LCW3_MERGE
+  // the whole r = 4 / r = 3 tables from their staged halves (read after the
+  // staging barrier, used after the next re-layout's barriers)
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int y = t + e * kThreads;
+    s_tab[tab_off(kT4) + y] = cmul(s_tab[tab_off(kT4a) + (y & 31)], s_tab[tab_off(kT4b) + (y >> 4)]);
+  }
+  if (t < 128) s_tab[tab_off(kT3) + t] = cmul(s_tab[tab_off(kT3a) + (t & 15)], s_tab[tab_off(kT3b) + (t >> 3)]);
+#endif
   xch(LCW3_L(kX1f), LCW3_L(kX2));
   // ---- X2: l1 on m4 m3 m2 m1, z0 p1 (swapped in), D5, l2 ----
   kick(C0{}, C1{}, LCW3_S(m4));
@@ -1164,7 +1183,11 @@ __global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArg
   kick(C3{}, C2{}, LCW3_S(m3));
   swap_reg_lane<2, 16>(v);  // register bit 2: m4 (lane bit 4: p4)
   kick(C2{}, C2{}, LCW3_S(m4));
+#ifdef DTC_LCW3_MERGE
+  diag1(LCW3_L(kX3e), LCW3_L(kT4));
+#else
   diag2(LCW3_L(kX3e), LCW3_L(kT4a), LCW3_L(kT4b));
+#endif
   kick(C0{}, C3{}, LCW3_S(p2));
   kick(C1{}, C3{}, LCW3_S(p3));
   kick(C3{}, C3{}, LCW3_S(m3));
@@ -1174,7 +1197,11 @@ __global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArg
   kick(C1{}, C3{}, LCW3_S(m1));
   kick(C2{}, C3{}, LCW3_S(z0));
   kick(C3{}, C3{}, LCW3_S(p1));
+#ifdef DTC_LCW3_MERGE
+  diag1(LCW3_L(kX4), LCW3_L(kT3));
+#else
   diag2(LCW3_L(kX4), LCW3_L(kT3a), LCW3_L(kT3b));
+#endif
   kick(C0{}, C4{}, LCW3_S(m2));
   kick(C1{}, C4{}, LCW3_S(m1));
   kick(C2{}, C4{}, LCW3_S(z0));

@@ -393,7 +393,12 @@ def test_lcw3_c2_form(pkg, monkeypatch, L, T, pol, state, toff, g, p):
     w8, _, _ = run(["DTC_NO_LCW"])
     for o in (w10, w8):
         assert np.abs(got["echo"] - o["echo"]).max() < 1e-12
-        assert np.abs(got["fwd"] - o["fwd"]).max() == 0.0
+        # the forward pass that carries a chain's echo start is a dual pass in
+        # one schedule and a plain K-D-K in the other; the 8-site dual runs its
+        # kicks in Pauli-frame form and the plain 8-site pass in branch form
+        # (round 6), so the forward may differ by an ulp (as in
+        # test_echo_light_cone_end)
+        assert np.abs(got["fwd"] - o["fwd"]).max() < 1e-13
     assert c10["lcw3"] == 0
     if L <= 21:  # two site groups: the C2 chains' form
         assert counts["lcw3"] > 0, counts
