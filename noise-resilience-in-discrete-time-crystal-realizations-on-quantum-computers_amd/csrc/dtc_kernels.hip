@@ -685,6 +685,12 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // three-per-CU energy passes: per wave, X point (post, pre), nibble, the
   // eight lane partials of the nibble's four sites (x_now)
   __shared__ double s_xpart[(SPLIT && MC == 3) ? kThreads / 64 : 1][2][3][32];
+  // device-like noise: the deferred Kraus diagonals' nibble tables (record set
+  // R / R2, pre / post layer, nibble, its 16 bit patterns): prod over the
+  // nibble's four sites of rho_{k, x_k}, staged once per workgroup (rho_apply)
+  constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
+  constexpr int kRhoSets = DUAL ? 2 : 1;
+  __shared__ double s_rho[kRho ? kRhoSets * 96 : 1];
 
   const int t = threadIdx.x;
   const int c = A.c, s = A.s;
@@ -817,6 +823,23 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   // flight.  Explicit, so no use of them waits for the tile.
   static_assert(kRegs == 16, "vmcnt immediate assumes 16 tile loads");
   __builtin_amdgcn_s_waitcnt(0x4F70);
+  if constexpr (kRho) {
+    // entry e = ((set * 2 + layer) * 3 + nibble) * 16 + pattern, one per thread
+    // (a nibble without kicks: 1); made visible by the first exchange's barrier
+    // or by the diagonal's (below), before the first rho_apply
+    if (t < kRhoSets * 96) {
+      const int set = t / 96, layer = (t / 48) & 1, nib = (t >> 4) % 3, pat = t & 15;
+      double pr = 1.0;
+      if ((NIBS >> nib) & 1) {
+        const double* rd =
+            (const double*)((set ? A.recs2 : A.recs) + b * kRecPerState) + 8 * (layer * kTileBits + 4 * nib);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pr *= rd[8 * q + (((pat >> q) & 1) ? 4 : 3)];
+      }
+      s_rho[t] = pr;
+    }
+    if constexpr (!RP::diag && !(RP::pre && (RP::n0 || RP::nO))) __syncthreads();
+  }
   // Pauli-frame kicks (frame12_records): the unitary families' passes over
   // nibble sets 6 and 7 that measure no X in flight run one butterfly per
   // kick; the frame's X bits leave through the re-layouts' write slots
@@ -1180,35 +1203,22 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   const bool x_pre = MC == 3 && (A.meas_parts & kPartXPre);
   const bool x_post = MC == 3 && (A.meas_parts & kPartXPost);
   // device-like noise: a kick layer's deferred Kraus factors (SiteMat),
-  // prod over the tile bits k of rho_{k, x_k}, in layout LAY (records rec0 ..)
-  constexpr bool kRho = KIND == kKindRXU || KIND == kKindRYU;
-  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], const auto& Rr) {
+  // prod over the tile bits k of rho_{k, x_k}, in layout LAY: the lane
+  // nibbles' factors from the staged nibble tables (one LDS read each), times
+  // the register nibble's 16 (uniform reads); record set 0 = R, 1 = R2
+  auto rho_apply = [&](auto lay_tag, int rec0, double2 (&x)[kRegs], int set) {
     constexpr int LAY = decltype(lay_tag)::value;
     const int y = ybase<LAY>(t);
+    const double* T = s_rho + (set * 2 + (rec0 ? 1 : 0)) * 48;
     double rt = 1.0;
 #pragma unroll
-    for (int k = 0; k < kTileBits; ++k) {
-      if (k >= 4 * LAY && k < 4 * LAY + 4) continue;  // register bits
-      if (!((NIBS >> (k >> 2)) & 1)) continue;        // no kicks: rho = 1
-      rt *= ((y >> k) & 1) ? Rr.d(rec0 + k, 4) : Rr.d(rec0 + k, 3);
-    }
-    double f[kRegs];
-    f[0] = rt;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool on = (NIBS >> LAY) & 1;
-      const double r0 = on ? Rr.d(rec0 + 4 * LAY + q, 3) : 1.0;
-      const double r1 = on ? Rr.d(rec0 + 4 * LAY + q, 4) : 1.0;
-#pragma unroll
-      for (int r = 0; r < (1 << q); ++r) {
-        f[r | (1 << q)] = f[r] * r1;
-        f[r] *= r0;
-      }
-    }
+    for (int n = 0; n < 3; ++n)
+      if (n != LAY && ((NIBS >> n) & 1)) rt *= T[16 * n + ((y >> (4 * n)) & 15)];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      x[r].x *= f[r];
-      x[r].y *= f[r];
+      const double f = ((NIBS >> LAY) & 1) ? rt * T[16 * LAY + r] : rt;
+      x[r].x *= f;
+      x[r].y *= f;
     }
   };
 
@@ -1264,7 +1274,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   if constexpr (kCo) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
-    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
+    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, 0);
     if constexpr (FR) zflush(std::integral_constant<int, RP::d_lay>{}, w, fzw2 & (kTile - 1));
   } else if constexpr (DUAL) {
     // the echo branch: E = K'_1 K_p (input) -- the forward pass's D, its
@@ -1273,7 +1283,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int r = 0; r < kRegs; ++r) w[r] = v[r];
     // (device-like noise, a forward K-D: E = K'_1 D^* D K_p (input) -- the
     // pre-kick's deferred Kraus diagonal first, K'_1's before the store)
-    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, R);
+    if constexpr (kRho) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, w, 0);
     if constexpr (RP::nO) {
       xch_tile<SPLIT, RP::d_lay, RP::O>(w, s_tile, s_half, t);
       apply_nibble<RP::O, KIND, qm(RP::O)>(w, R2, kTileBits);
@@ -1287,7 +1297,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND, qm(RP::IO)>(w, R2, kTileBits);
     }
     xch_tile<SPLIT, RP::pIO, RP::IO>(w, s_tile, s_half, t);
-    if constexpr (kRho) rho_apply(LIO{}, kTileBits, w, R2);
+    if constexpr (kRho) rho_apply(LIO{}, kTileBits, w, 1);
     // the branch's global factor: i^k w of K_p and of K'_1
     const double2 gE = make_double2(R2.d(kRecTotal, 0), R2.d(kRecTotal, 1));
     char* d2 = (char*)(A.dst2 + sbase);
@@ -1301,7 +1311,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     // reading in the branch's last one
     __syncthreads();
   }
-  if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, v, R);
+  if constexpr (kRho && RP::pre) rho_apply(std::integral_constant<int, RP::d_lay>{}, 0, v, 0);
   if constexpr (!RP::diag) {
     // no diagonal to carry the kicks' global factor (kick-only pass: no
     // post-kick, so applying it here, before any measurement, is exact)
@@ -1344,8 +1354,8 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     exchange_split2<RP::pIO, RP::IO>(v, w, s_half, s_half2, t, fxm(RP::x4 - 1), fxm(RP::x4),
                                      fxm2(RP::x4 - 1), fxm2(RP::x4));
     if constexpr (kRho) {
-      rho_apply(LIO{}, kTileBits, v, R);
-      rho_apply(LIO{}, kTileBits, w, R2);
+      rho_apply(LIO{}, kTileBits, v, 0);
+      rho_apply(LIO{}, kTileBits, w, 1);
     }
   } else if constexpr (RP::post) {
     double sc = inv_w2_mid;
@@ -1367,7 +1377,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
       apply_nibble<RP::IO, KIND, qm(RP::IO), FR>(v, R, kTileBits);
     }
     xch_f(std::integral_constant<int, RP::pIO>{}, std::integral_constant<int, RP::IO>{}, RP::x4);
-    if constexpr (kRho) rho_apply(LIO{}, kTileBits, v, R);
+    if constexpr (kRho) rho_apply(LIO{}, kTileBits, v, 0);
   } else {
     xch_f(std::integral_constant<int, RP::d_lay>{}, std::integral_constant<int, RP::IO>{}, RP::x5);
   }
