@@ -1387,12 +1387,24 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   DTC_TS(5);
 
   char* dst = (char*)(A.dst + sbase);
+  // the stores' lane offset: recomputed from an opaque copy of t in the
+  // instantiations that spilled it (three per CU, 168 VGPRs: the device-noise,
+  // per-site and 8-site passes kept the load offset alive through the pass,
+  // an 8-byte scratch spill per thread, r6f); the others keep the load's
+  constexpr bool kRematOfs = SPLIT && (kRho || MC == 2 || NIBS != 7);
+  int64_t sofs64 = vofs64;
+  if constexpr (kRematOfs) {
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    sofs64 = octet_spread(M.rel(ybase<RP::IO>(tt)), og) << 4;
+  }
+  const uint32_t sofs = (uint32_t)sofs64;
   if constexpr (NS) {
     // measurement-only pass (the last of an echo chain): nothing to write
   } else if (ofs32) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      char* a = dst + tile_ofs(r) + vofs;
+      char* a = dst + tile_ofs(r) + sofs;
       if constexpr (kNt & 2) {
         d2v w = {v[r].x, v[r].y};
         __builtin_nontemporal_store(w, (d2v*)a);
@@ -1403,7 +1415,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
   } else {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-      char* a = dst + tile_ofs(r) + vofs64;
+      char* a = dst + tile_ofs(r) + sofs64;
       if constexpr (kNt & 2) {
         d2v w = {v[r].x, v[r].y};
         __builtin_nontemporal_store(w, (d2v*)a);
@@ -1422,7 +1434,7 @@ __device__ __forceinline__ void pass_body(const PassArgs& A) {
     for (int r = 0; r < kRegs; ++r) {
       const double2 u = cmul(w[r], gE);
       d2v x = {u.x, u.y};
-      __builtin_nontemporal_store(x, (d2v*)(d2 + tile_ofs(r) + (ofs32 ? (int64_t)vofs : vofs64)));
+      __builtin_nontemporal_store(x, (d2v*)(d2 + tile_ofs(r) + (ofs32 ? (int64_t)sofs : sofs64)));
     }
   }
   if constexpr (MC == 1) {

@@ -1234,10 +1234,15 @@ __global__ __launch_bounds__(kThreads, DTC_LCW3_WPS) void dtc_lcw3_final(PassArg
     s_red[wave][1] = z;
   }
   __syncthreads();
-  if (t < 2) {
+  // (an opaque copy of t: the compiler would otherwise keep the 8 t of the
+  // slot bases alive to here at the 128-VGPR cap -- a 4-byte spill per thread,
+  // 1 KB of scratch writes per workgroup, r6e)
+  int t2 = t;
+  asm volatile("" : "+v"(t2));
+  if (t2 < 2) {
     double acc = 0.0;
-    for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t];
-    A.partial[(b * n_tiles + tile) * A.n_obs + t] = acc;
+    for (int k = 0; k < kThreads / 64; ++k) acc += s_red[k][t2];
+    A.partial[(b * n_tiles + tile) * A.n_obs + t2] = acc;
   }
 }
 

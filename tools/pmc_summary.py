@@ -87,9 +87,12 @@ def main(prof, out, batch, L, bench_args=""):
             ("kdk_single", ("dtc_kdk_pass",), {"dtc_kdk_pass": 32.0}),
             ("kdk_dual", ("dtc_kdk_dual",), {"dtc_kdk_dual": 48.0}),
             ("hi_pass", ("dtc_kick_pass",), None),
-            ("lightcone_pass", ("dtc_lc_final",), None),
-            ("lightcone_wide_pass", ("dtc_lcw2_final", "dtc_lcw_final"), None),
-            ("lightcone_12site_pass", ("dtc_lcw3_final",), None)):
+            # (the light-cone ends read the state once and store only their
+            # per-tile partials: 16 B per amplitude whatever the counters show)
+            ("lightcone_pass", ("dtc_lc_final",), {"dtc_lc_final": 16.0}),
+            ("lightcone_wide_pass", ("dtc_lcw2_final", "dtc_lcw_final"),
+             {"dtc_lcw2_final": 16.0, "dtc_lcw_final": 16.0}),
+            ("lightcone_12site_pass", ("dtc_lcw3_final",), {"dtc_lcw3_final": 16.0})):
         r = one(names, per_amp)
         if r:
             res[key] = r
