@@ -16,7 +16,7 @@ for lib in "$@"; do
 import json, sys, pandas as pd
 d = json.load(open(sys.argv[1] + ".json"))
 k = pd.read_csv(sys.argv[1] + "/kt_kernel_stats.csv")
-k = k[k.Name.str.contains("kdk|lcw|lc_final|pass13")]
+k = k[k.Name.str.contains("kdk|lcw|lc_final|pass13|kick_swap|kick_pass")]
 print(sys.argv[2], round(d["value"]), round(d["roofline"]["achieved"]),
       " ".join(f"{r.Name.split('dtc_')[-1].split('(')[0].replace(' ', '')}={r.AverageNs / 1e6:.4f}" for r in k.itertuples()))
 PY
