@@ -1890,13 +1890,18 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_kick_swap_pass(PassArgs A, in
     const d2v x = __builtin_nontemporal_load((const d2v*)(p1 + tile_ofs(rr) + vofs));
     v[rr] = make_double2(x.x, x.y);
   }
-  if (b2 != b1) {
+  // the partner tile, loaded after v's kicks (behind v's stores): with its
+  // loads issued up front both tiles were live through v's kicks and the
+  // 256-VGPR budget spilled 20-100 B per thread (r6h: 11.62 -> 11.28 ms)
+  auto load_w = [&]() {
+    if (b2 != b1) {
 #pragma unroll
-    for (int rr = 0; rr < kRegs; ++rr) {
-      const d2v x = __builtin_nontemporal_load((const d2v*)(p2 + tile_ofs(rr) + vofs));
-      w[rr] = make_double2(x.x, x.y);
+      for (int rr = 0; rr < kRegs; ++rr) {
+        const d2v x = __builtin_nontemporal_load((const d2v*)(p2 + tile_ofs(rr) + vofs));
+        w[rr] = make_double2(x.x, x.y);
+      }
     }
-  }
+  };
   const double2 gph = make_double2(R.d(kRecTotal, 0), R.d(kRecTotal, 1));
   // the kick-only pass of pass_body: rounds IO -> 0 -> O, the global factor,
   // back to the IO layout
@@ -1923,6 +1928,7 @@ __global__ __launch_bounds__(kThreads, 2) void dtc_kick_swap_pass(PassArgs A, in
     }
   };
   kick(v);
+  load_w();
   store(v, p2);  // (r, c) -> (c, r); the diagonal piece in place
   if (b2 != b1) {  // uniform across the workgroup
     // w's first re-layout writes slots other threads may still be reading in
