@@ -15,6 +15,9 @@
 #   stage              copy this call's PMC summaries (gpurun_out/<tag>*_pmc*.json) into
 #                      profiles/ of the box's copy, so later bench steps cite them
 #   exec:<file>        run gpu_bin/<file> (a probe built in the container) -> <tag>_<file>.txt
+#   libtests:<lib>:<k> pytest -m gpu -k <k> against devlib/<lib>.so (a variant's parity before
+#                      its A/B) -> <tag>_par_<lib>.txt
+#   configs            every non-C2 line once (tools/measure_configs.sh)
 set -o pipefail
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -61,6 +64,12 @@ for step in "$@"; do
       f=${step#exec:}
       timeout -k 10 300 gpu_bin/$f > $O/${TAG}_$f.txt 2>&1 || { tail -5 $O/${TAG}_$f.txt; exit 1; }
       cat $O/${TAG}_$f.txt ;;
+    libtests:*)
+      IFS=: read -r _ lib k <<< "$step"
+      DTC_LIB=$R/devlib/$lib.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$k" > $O/${TAG}_par_$lib.txt 2>&1 || { tail -20 $O/${TAG}_par_$lib.txt; exit 1; }
+      tail -1 $O/${TAG}_par_$lib.txt ;;
+    configs)
+      bash tools/measure_configs.sh $TAG || exit 1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
